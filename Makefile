@@ -1,0 +1,44 @@
+# Build of the MI355X (gfx950) solve loop.  Driven by __graft_entry__.build()
+# (`make -j8 all`); everything lands in-tree so it travels to the GPU box.
+#   libfrecsys_hip.so  -- HIP kernels + C-ABI (include/frecsys_hip.h)
+#   run_model          -- reference-compatible CLI (C++ host over the C-ABI)
+#   liboracle.so       -- CPU restatement, TEST INFRASTRUCTURE ONLY
+PKG      := safer2-recommender_amd
+CSRC     := $(PKG)/csrc
+OBJ      := $(PKG)/build
+LIB      := $(PKG)/frecsys_hip/libfrecsys_hip.so
+ORACLE   := oracle/liboracle.so
+RUNMODEL := $(PKG)/bin/run_model
+ARCH     ?= gfx950
+HIPCC    ?= /opt/rocm/bin/hipcc
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
+CXXFLAGS := -O3 -std=c++17 -Wall -I include -I $(PKG)/include -pthread
+
+HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/gramian.hip $(CSRC)/loss.hip $(CSRC)/capi.hip
+HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
+HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h include/frecsys_hip.h
+
+.PHONY: all lib oracle run_model clean
+all: lib oracle run_model
+lib: $(LIB)
+oracle: $(ORACLE)
+run_model: $(RUNMODEL)
+
+$(OBJ)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS) -lrccl
+
+$(ORACLE): oracle/frecsys_oracle.c oracle/frecsys_oracle.h
+	gcc -O3 -march=native -std=c11 -fPIC -shared -Wall -o $@ oracle/frecsys_oracle.c -lpthread -lm
+
+FRECSYS_HDRS := $(wildcard $(PKG)/include/frecsys/*.h)
+$(RUNMODEL): $(PKG)/tools/run_model.cc $(FRECSYS_HDRS) include/frecsys_hip.h $(LIB)
+	@mkdir -p $(PKG)/bin
+	g++ $(CXXFLAGS) -o $@ $(PKG)/tools/run_model.cc -L$(PKG)/frecsys_hip -lfrecsys_hip \
+	    -Wl,-rpath,'$$ORIGIN/../frecsys_hip'
+
+clean:
+	rm -rf $(OBJ) $(LIB) $(ORACLE) $(PKG)/bin

@@ -1,0 +1,172 @@
+/*
+ * frecsys_hip.h -- C-ABI of libfrecsys_hip.so, the MI355X (gfx950) solve
+ * loop behind iALS / ERM-MF / CVaR-MF / SAFER2.
+ *
+ * Plain C types only (no torch / HIP / RCCL types).  Every call is
+ * synchronous on return (the reference's Step* functions block until all
+ * threads join, ials.h:359-361) and returns FRECSYS_OK (0) or an error code;
+ * frecsys_last_error() gives the message.  The library owns every device
+ * buffer (embeddings, Gramians, CSR, workspaces); they stay resident in HBM
+ * across epochs.  Host pointers passed in are never retained after a call.
+ *
+ * Which reference interface each entry point replaces (reference paths are
+ * relative to riktor/safer2-recommender):
+ *
+ *   frecsys_ctx_create / destroy  -- the model ctor's allocation of
+ *       user_embedding_ / item_embedding_ / item_gramian_
+ *       (ials.h:39-45, safer2.h:37-48, erm_mf.h:36-44, cvar_mf.h:36-43)
+ *   frecsys_load_csr              -- Dataset::by_user()/by_item()
+ *       (dataset.h:27-32, 83-92): the per-entity SpVector histories, as CSR
+ *       rows kept in file order
+ *   frecsys_set/get_embeddings    -- init_matrix writes (recommender.h:61-67)
+ *       and item_embedding() reads (ials.h:410-412)
+ *   frecsys_init_embeddings       -- std::mt19937 + normal_distribution<float>
+ *       init of U then V (ials.h:47-51, recommender.h:61-67), seeded
+ *   frecsys_gramian               -- `X.transpose() * X` (ials.h:321,
+ *       ials.h:371, safer2.h:55, safer2.h:294-295) and the weighted
+ *       `U^T (U .* omega)` (safer2.h:504-509, erm_mf.h:462-467,
+ *       cvar_mf.h:484-489)
+ *   frecsys_solve_side            -- Step / StepU / StepV / StepU_eval with
+ *       their static per-entity Project / ProjectU / ProjectV /
+ *       ProjectU_eval (ials.h:88-144 + 317-365; safer2.h:104-221 + 437-555;
+ *       erm_mf.h:91-210 + 397-513; cvar_mf.h:88-229 + 427-538 + 645-692)
+ *   frecsys_user_loss             -- ComputeUserLoss / ComputeLoss
+ *       (ials.h:70-86 + 367-408; safer2.h:85-101 + 558-596)
+ *   frecsys_comm_* / frecsys_partition -- new: the reference has no
+ *       multi-device path; these shard the entity loop of the Step* drivers
+ *       (safer2.h:447-487) across one process per GPU (RCCL over xGMI).
+ */
+#ifndef FRECSYS_HIP_H_
+#define FRECSYS_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define FRECSYS_OK 0
+#define FRECSYS_ERR_INVALID 1     /* bad argument / state */
+#define FRECSYS_ERR_HIP 2         /* HIP runtime error */
+#define FRECSYS_ERR_RCCL 3        /* RCCL error */
+#define FRECSYS_ERR_NOT_SPD 4     /* LLT failed (reference: assert, ials.h:141);
+                                     entity id via frecsys_last_error_entity */
+#define FRECSYS_ERR_NAN 5         /* NaN detected (reference: LOG(ERROR) + exit) */
+#define FRECSYS_ERR_UNSUPPORTED 6 /* e.g. dim beyond the kernels built */
+#define FRECSYS_ERR_NO_DEVICE 7   /* no HIP device visible */
+
+/* ---- sides ---- */
+#define FRECSYS_SIDE_USER 0 /* train by_user: rows = users, cols = items */
+#define FRECSYS_SIDE_ITEM 1 /* train by_item: rows = items, cols = users */
+#define FRECSYS_SIDE_EVAL 2 /* fold-in users (EvaluateDataset, ials.h:148-174);
+                               rows = compacted eval users, cols = items */
+
+/* ---- per-entity solve kinds ---- */
+#define FRECSYS_KIND_IALS 0        /* ials.h:88-144 */
+#define FRECSYS_KIND_WEIGHTED_U 1  /* safer2.h:104-163, erm_mf.h:91-151,
+                                      cvar_mf.h:182-229 (ProjectU_eval) */
+#define FRECSYS_KIND_WEIGHTED_V 2  /* safer2.h:166-221, erm_mf.h:153-210 */
+#define FRECSYS_KIND_CVAR_GRAD_U 3 /* cvar_mf.h:88-134 */
+#define FRECSYS_KIND_CVAR_GRAD_V 4 /* cvar_mf.h:136-180 */
+
+typedef struct frecsys_ctx frecsys_ctx;
+
+typedef struct {
+  int32_t dim;           /* embedding dimension (reference --dim) */
+  int32_t device;        /* HIP device ordinal; -1 = current device */
+  int32_t parity_quirks; /* 1: reproduce reference quirks */
+  int32_t reserved;
+  int64_t n_users;       /* max_user + 1 (run_model.cc:240) */
+  int64_t n_items;       /* max_item + 1 */
+} frecsys_config;
+
+typedef struct {
+  int32_t kind;            /* FRECSYS_KIND_* */
+  float reg;               /* l2_reg */
+  float reg_exp;           /* l2_reg_exp (iALS only, ials.h:312-314) */
+  float unobserved_weight; /* uobs_weight */
+  float alpha;             /* alpha (ItemRegularizationValue, safer2.h:430) */
+  float stepsize;          /* CVaR-MF eta (cvar_mf.h:133) */
+  int32_t from_snapshot;   /* 1: X = snapshot of the other side (CVaR StepV
+                              uses the pre-step U, cvar_mf.h:282,294) */
+  int32_t reserved;
+  const float* entity_weight; /* host [rows of side]: omega_u (WEIGHTED_U,
+                                 CVAR_GRAD_U); NULL -> 1 */
+  const float* entity_reg;    /* host [rows of side]: item_reg_[v]
+                                 (WEIGHTED_V, CVAR_GRAD_V) */
+  const float* other_weight;  /* host [rows of other side]: nu_u =
+                                 omega_u / |H_u| (WEIGHTED_V, CVAR_GRAD_V) */
+} frecsys_solve_params;
+
+/* ---- context ---- */
+int frecsys_device_count(int32_t* n);
+int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out);
+void frecsys_ctx_destroy(frecsys_ctx* ctx);
+/* Message of the last error on ctx (ctx may be NULL: last global error). */
+const char* frecsys_last_error(const frecsys_ctx* ctx);
+/* Entity (row of the side) of the last FRECSYS_ERR_NOT_SPD, or -1. */
+int64_t frecsys_last_error_entity(const frecsys_ctx* ctx);
+/* Padded leading dimension used on device (dim rounded up). */
+int32_t frecsys_padded_dim(int32_t dim);
+
+/* ---- multi-GPU (one process per GPU) ---- */
+/* Host-only: contiguous nnz-balanced split of rows into nparts ranges,
+ * bounds[0]=0 .. bounds[nparts]=n_rows (safe to call without a GPU). */
+int frecsys_partition(int64_t n_rows, const int64_t* row_ptr, int32_t nparts,
+                      int64_t* bounds);
+/* RCCL unique id (128 bytes) -- call on rank 0, broadcast to the others. */
+int frecsys_comm_unique_id(uint8_t id[128]);
+int frecsys_comm_init(frecsys_ctx* ctx, int32_t world, int32_t rank,
+                      const uint8_t id[128]);
+/* Row range [lo, hi) of `side` owned by this rank (after load_csr). */
+int frecsys_shard_range(const frecsys_ctx* ctx, int32_t side, int64_t* lo,
+                        int64_t* hi);
+
+/* ---- data ---- */
+int frecsys_load_csr(frecsys_ctx* ctx, int32_t side, int64_t n_rows,
+                     const int64_t* row_ptr, const int32_t* col);
+int frecsys_set_embeddings(frecsys_ctx* ctx, int32_t side, const float* host,
+                           int64_t ld);
+int frecsys_get_embeddings(frecsys_ctx* ctx, int32_t side, float* host,
+                           int64_t ld);
+/* Seeded init of U then V, identical to std::mt19937{seed} +
+ * std::normal_distribution<float>(0, stdev/sqrt(dim)) per matrix. */
+int frecsys_init_embeddings(frecsys_ctx* ctx, uint32_t seed, float stdev);
+/* Copy the current embeddings of side into its snapshot slot. */
+int frecsys_snapshot(frecsys_ctx* ctx, int32_t side);
+
+/* ---- compute ---- */
+/* G[side] = X^T diag(w) X over all rows of side's embeddings (or of its
+ * snapshot); each rank sums its shard, then RCCL all-reduce.  weights: host
+ * [rows of side] or NULL.  host_out (dim x dim, row-major) may be NULL. */
+int frecsys_gramian(frecsys_ctx* ctx, int32_t side, const float* weights,
+                    int32_t from_snapshot, float* host_out);
+/* Solve every row of `side` owned by this rank against the other side's
+ * embeddings and G[other side]; rows with an empty history are left
+ * untouched.  USER/ITEM results are then all-gathered across ranks.  EVAL
+ * solves against ITEM and writes the EVAL embeddings. */
+int frecsys_solve_side(frecsys_ctx* ctx, int32_t side,
+                       const frecsys_solve_params* params);
+/* Per-user loss over `side` (USER or EVAL) rows against ITEM embeddings and
+ * G[ITEM]: (1/h) sum (x.u - 1)^2 + beta u^T G u, halved if half != 0.
+ * Rows with empty history get 0.  host_out [rows] may be NULL (result kept
+ * on device); for USER it is gathered across ranks first. */
+int frecsys_user_loss(frecsys_ctx* ctx, int32_t side, float beta, int32_t half,
+                      float* host_out);
+/* Block until all queued device work is done (all calls already do). */
+int frecsys_synchronize(frecsys_ctx* ctx);
+
+/* ---- profiling hooks (bench.py) ----
+ * Kernel time accumulated with HIP events recorded on the library's own
+ * stream around each launch of kernel class `what` ("solve_user",
+ * "solve_item", "solve_eval", "gramian", "user_loss", "allgather",
+ * "allreduce") since the last frecsys_timing_reset. */
+int frecsys_timing(const frecsys_ctx* ctx, const char* what, double* total_ms,
+                   int64_t* launches);
+int frecsys_timing_reset(frecsys_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FRECSYS_HIP_H_ */

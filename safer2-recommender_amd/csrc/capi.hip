@@ -1,0 +1,656 @@
+// capi.hip -- host side of libfrecsys_hip.so: the C-ABI declared in
+// include/frecsys_hip.h.  Owns the device state of one process (one GPU):
+// embeddings (row-major, padded leading dim), Gramians, CSR of each side,
+// workspaces, the RCCL communicator, and the HIP stream everything runs on.
+//
+// Sharding (one process per GPU): every rank keeps full replicas of U and V
+// (they fit HBM at every configured size) and owns a contiguous nnz-balanced
+// range of users and of items.  A half-step is
+//   partial G over own rows -> ncclAllReduce -> solve own rows ->
+//   grouped ncclBroadcast of every rank's rows (an all-gather with uneven
+//   counts, in place).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/frecsys_hip.h"
+#include "kernels.h"
+
+using namespace frecsys_hip;
+
+namespace {
+
+std::string g_last_error;
+
+struct Timer {
+  double total_ms = 0.0;
+  int64_t launches = 0;
+};
+
+}  // namespace
+
+struct frecsys_ctx {
+  int dim = 0, Dp = 0, device = 0, quirks = 1;
+  int64_t n[3] = {0, 0, 0};
+  hipStream_t stream = nullptr;
+  float* emb[3] = {nullptr, nullptr, nullptr};
+  float* snap[2] = {nullptr, nullptr};
+  float* gram[2] = {nullptr, nullptr};
+  int64_t* rp[3] = {nullptr, nullptr, nullptr};
+  int32_t* col[3] = {nullptr, nullptr, nullptr};
+  int64_t nnz[3] = {0, 0, 0};
+  std::vector<int64_t> host_rp[2];
+  std::vector<int64_t> bounds[2];
+  // per-entity vectors (device)
+  float* d_entity_weight = nullptr;
+  size_t cap_entity_weight = 0;
+  float* d_entity_reg = nullptr;
+  size_t cap_entity_reg = 0;
+  float* d_other_weight = nullptr;
+  size_t cap_other_weight = 0;
+  float* d_gram_w = nullptr;
+  size_t cap_gram_w = 0;
+  float* d_partials = nullptr;
+  size_t cap_partials = 0;
+  float* d_loss = nullptr;
+  size_t cap_loss = 0;
+  unsigned long long* d_fail = nullptr;
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0;
+  std::string err;
+  int64_t err_entity = -1;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::map<std::string, Timer> timers;
+};
+
+namespace {
+
+int fail(frecsys_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(c, expr)                                                            \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess)                                                           \
+      return fail((c), FRECSYS_ERR_HIP,                                             \
+                  std::string(#expr) + ": " + hipGetErrorString(_e));               \
+  } while (0)
+
+#define NCCL_TRY(c, expr)                                                           \
+  do {                                                                              \
+    ncclResult_t _r = (expr);                                                       \
+    if (_r != ncclSuccess)                                                          \
+      return fail((c), FRECSYS_ERR_RCCL,                                            \
+                  std::string(#expr) + ": " + ncclGetErrorString(_r));              \
+  } while (0)
+
+template <typename T>
+int ensure(frecsys_ctx* c, T** p, size_t* cap, size_t count) {
+  if (*cap >= count && *p) return FRECSYS_OK;
+  if (*p) HIP_TRY(c, hipFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  HIP_TRY(c, hipMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1)));
+  *cap = count;
+  return FRECSYS_OK;
+}
+
+bool valid_side(int side) { return side >= 0 && side <= 2; }
+
+// Contiguous nnz-balanced split: rank r gets rows whose prefix nnz falls in
+// [r*nnz/P, (r+1)*nnz/P).
+void partition_rows(int64_t n_rows, const int64_t* row_ptr, int parts, int64_t* bounds) {
+  const int64_t nnz = row_ptr[n_rows] - row_ptr[0];
+  bounds[0] = 0;
+  for (int r = 1; r < parts; ++r) {
+    const int64_t target = row_ptr[0] + (nnz * r) / parts;
+    const int64_t* it = std::lower_bound(row_ptr, row_ptr + n_rows + 1, target);
+    int64_t b = it - row_ptr;
+    if (b < bounds[r - 1]) b = bounds[r - 1];
+    if (b > n_rows) b = n_rows;
+    bounds[r] = b;
+  }
+  bounds[parts] = n_rows;
+}
+
+void refresh_bounds(frecsys_ctx* c, int side) {
+  if (side > 1) return;
+  c->bounds[side].assign(c->world + 1, 0);
+  if (!c->host_rp[side].empty()) {
+    partition_rows(c->n[side], c->host_rp[side].data(), c->world, c->bounds[side].data());
+  } else {
+    for (int r = 0; r <= c->world; ++r) c->bounds[side][r] = c->n[side] * r / c->world;
+  }
+}
+
+void shard(const frecsys_ctx* c, int side, int64_t* lo, int64_t* hi) {
+  if (side > 1 || c->world == 1 || c->bounds[side].empty()) {
+    *lo = 0;
+    *hi = c->n[side];
+    return;
+  }
+  *lo = c->bounds[side][c->rank];
+  *hi = c->bounds[side][c->rank + 1];
+}
+
+// Row-range all-gather of a [rows x ld] float matrix (uneven per-rank
+// counts): every rank broadcasts its own range in place.
+int allgather_rows(frecsys_ctx* c, float* base, int side, int64_t ld) {
+  if (c->world == 1) return FRECSYS_OK;
+  NCCL_TRY(c, ncclGroupStart());
+  for (int r = 0; r < c->world; ++r) {
+    const int64_t lo = c->bounds[side][r], hi = c->bounds[side][r + 1];
+    const size_t cnt = (size_t)(hi - lo) * ld;
+    if (cnt == 0) continue;
+    float* p = base + lo * ld;
+    NCCL_TRY(c, ncclBroadcast(p, p, cnt, ncclFloat, r, c->comm, c->stream));
+  }
+  NCCL_TRY(c, ncclGroupEnd());
+  return FRECSYS_OK;
+}
+
+int upload(frecsys_ctx* c, float** dptr, size_t* cap, const float* host, size_t n) {
+  int rc = ensure(c, dptr, cap, n);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemcpyAsync(*dptr, host, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  return FRECSYS_OK;
+}
+
+struct ScopedTimer {
+  frecsys_ctx* c;
+  const char* name;
+  ScopedTimer(frecsys_ctx* c_, const char* n_) : c(c_), name(n_) {
+    (void)hipEventRecord(c->ev0, c->stream);
+  }
+  // Stops the timer: synchronises on the end event and accumulates.
+  void stop() {
+    (void)hipEventRecord(c->ev1, c->stream);
+    (void)hipEventSynchronize(c->ev1);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) {
+      Timer& t = c->timers[name];
+      t.total_ms += ms;
+      t.launches += 1;
+    }
+  }
+};
+
+// Restatement of libstdc++ std::normal_distribution<float>::operator()
+// (Marsaglia polar; bits/random.tcc) over std::generate_canonical<float,24>
+// of std::mt19937, with FMA contraction off so x*x + y*y rounds like the
+// un-fused library code.  Drives the seeded init of init_matrix
+// (recommender.h:61-67).
+#pragma clang fp contract(off)
+struct NormalF {
+  bool saved_available = false;
+  float saved = 0.f;
+  static float canonical(std::mt19937& g) {
+    float s = (float)g();
+    float r = s / 4294967296.0f;
+    if (r >= 1.0f) r = std::nextafter(1.0f, 0.0f);
+    return r;
+  }
+  float operator()(std::mt19937& g, float mean, float stddev) {
+    float ret;
+    if (saved_available) {
+      saved_available = false;
+      ret = saved;
+    } else {
+      float x, y, r2;
+      do {
+        x = (float)((double)(2.0f * canonical(g)) - 1.0);
+        y = (float)((double)(2.0f * canonical(g)) - 1.0);
+        r2 = x * x + y * y;
+      } while (r2 > 1.0 || r2 == 0.0);
+      const float mult = std::sqrt(-2 * std::log(r2) / r2);
+      saved = x * mult;
+      saved_available = true;
+      ret = y * mult;
+    }
+    return ret * stddev + mean;
+  }
+};
+#pragma clang fp contract(on)
+
+}  // namespace
+
+extern "C" {
+
+int32_t frecsys_padded_dim(int32_t dim) { return padded_dim(dim); }
+
+int frecsys_device_count(int32_t* n) {
+  int cnt = 0;
+  hipError_t e = hipGetDeviceCount(&cnt);
+  if (e != hipSuccess) {
+    *n = 0;
+    return fail(nullptr, FRECSYS_ERR_NO_DEVICE, hipGetErrorString(e));
+  }
+  *n = cnt;
+  return FRECSYS_OK;
+}
+
+const char* frecsys_last_error(const frecsys_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_last_error.c_str();
+}
+
+int64_t frecsys_last_error_entity(const frecsys_ctx* ctx) { return ctx ? ctx->err_entity : -1; }
+
+int frecsys_partition(int64_t n_rows, const int64_t* row_ptr, int32_t nparts, int64_t* bounds) {
+  if (n_rows < 0 || nparts <= 0 || !row_ptr || !bounds)
+    return fail(nullptr, FRECSYS_ERR_INVALID, "frecsys_partition: bad arguments");
+  partition_rows(n_rows, row_ptr, nparts, bounds);
+  return FRECSYS_OK;
+}
+
+int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
+  if (!cfg || !out) return fail(nullptr, FRECSYS_ERR_INVALID, "null argument");
+  *out = nullptr;
+  const int Dp = padded_dim(cfg->dim);
+  if (Dp == 0)
+    return fail(nullptr, FRECSYS_ERR_UNSUPPORTED,
+                "dim " + std::to_string(cfg->dim) + " not supported (1..256 built)");
+  if (cfg->n_users < 0 || cfg->n_items < 0)
+    return fail(nullptr, FRECSYS_ERR_INVALID, "negative entity counts");
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0)
+    return fail(nullptr, FRECSYS_ERR_NO_DEVICE, "no HIP device visible");
+  auto* c = new frecsys_ctx();
+  c->dim = cfg->dim;
+  c->Dp = Dp;
+  c->quirks = cfg->parity_quirks;
+  c->n[0] = cfg->n_users;
+  c->n[1] = cfg->n_items;
+  if (cfg->device >= 0) {
+    c->device = cfg->device;
+  } else {
+    (void)hipGetDevice(&c->device);
+  }
+  auto bail = [&](int rc) {
+    g_last_error = c->err;
+    frecsys_ctx_destroy(c);
+    return rc;
+  };
+  if (hipSetDevice(c->device) != hipSuccess)
+    return bail(fail(c, FRECSYS_ERR_NO_DEVICE, "hipSetDevice failed"));
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed"));
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
+    return bail(fail(c, FRECSYS_ERR_HIP, "hipEventCreate failed"));
+  for (int s = 0; s < 2; ++s) {
+    const size_t rows = (size_t)std::max<int64_t>(c->n[s], 1);
+    if (hipMalloc((void**)&c->emb[s], sizeof(float) * rows * Dp) != hipSuccess ||
+        hipMalloc((void**)&c->gram[s], sizeof(float) * Dp * Dp) != hipSuccess)
+      return bail(fail(c, FRECSYS_ERR_HIP, "hipMalloc failed (embeddings)"));
+    (void)hipMemsetAsync(c->emb[s], 0, sizeof(float) * rows * Dp, c->stream);
+    (void)hipMemsetAsync(c->gram[s], 0, sizeof(float) * Dp * Dp, c->stream);
+  }
+  if (hipMalloc((void**)&c->d_fail, sizeof(unsigned long long)) != hipSuccess)
+    return bail(fail(c, FRECSYS_ERR_HIP, "hipMalloc failed"));
+  c->bounds[0] = {0, c->n[0]};
+  c->bounds[1] = {0, c->n[1]};
+  if (hipStreamSynchronize(c->stream) != hipSuccess)
+    return bail(fail(c, FRECSYS_ERR_HIP, "stream sync failed"));
+  *out = c;
+  return FRECSYS_OK;
+}
+
+void frecsys_ctx_destroy(frecsys_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  for (int s = 0; s < 3; ++s) {
+    if (c->emb[s]) (void)hipFree(c->emb[s]);
+    if (c->rp[s]) (void)hipFree(c->rp[s]);
+    if (c->col[s]) (void)hipFree(c->col[s]);
+  }
+  for (int s = 0; s < 2; ++s) {
+    if (c->snap[s]) (void)hipFree(c->snap[s]);
+    if (c->gram[s]) (void)hipFree(c->gram[s]);
+  }
+  for (float* p : {c->d_entity_weight, c->d_entity_reg, c->d_other_weight, c->d_gram_w,
+                   c->d_partials, c->d_loss})
+    if (p) (void)hipFree(p);
+  if (c->d_fail) (void)hipFree(c->d_fail);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int frecsys_comm_unique_id(uint8_t id[128]) {
+  ncclUniqueId uid;
+  ncclResult_t r = ncclGetUniqueId(&uid);
+  if (r != ncclSuccess) return fail(nullptr, FRECSYS_ERR_RCCL, ncclGetErrorString(r));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  std::memcpy(id, &uid, 128);
+  return FRECSYS_OK;
+}
+
+int frecsys_comm_init(frecsys_ctx* c, int32_t world, int32_t rank, const uint8_t id[128]) {
+  if (!c || world <= 0 || rank < 0 || rank >= world)
+    return fail(c, FRECSYS_ERR_INVALID, "frecsys_comm_init: bad rank/world");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->comm) {
+    ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  c->world = world;
+  c->rank = rank;
+  if (world > 1) {
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    NCCL_TRY(c, ncclCommInitRank(&c->comm, world, uid, rank));
+  }
+  refresh_bounds(c, 0);
+  refresh_bounds(c, 1);
+  return FRECSYS_OK;
+}
+
+int frecsys_shard_range(const frecsys_ctx* c, int32_t side, int64_t* lo, int64_t* hi) {
+  if (!c || !valid_side(side) || !lo || !hi) return FRECSYS_ERR_INVALID;
+  shard(c, side, lo, hi);
+  return FRECSYS_OK;
+}
+
+int frecsys_load_csr(frecsys_ctx* c, int32_t side, int64_t n_rows, const int64_t* row_ptr,
+                     const int32_t* col) {
+  if (!c || !valid_side(side) || !row_ptr || n_rows < 0)
+    return fail(c, FRECSYS_ERR_INVALID, "frecsys_load_csr: bad arguments");
+  if (side < 2 && n_rows != c->n[side])
+    return fail(c, FRECSYS_ERR_INVALID,
+                "frecsys_load_csr: row count " + std::to_string(n_rows) + " != " +
+                    std::to_string(c->n[side]));
+  const int64_t nnz = row_ptr[n_rows] - row_ptr[0];
+  if (row_ptr[0] != 0 || nnz < 0)
+    return fail(c, FRECSYS_ERR_INVALID, "frecsys_load_csr: row_ptr must start at 0");
+  const int other = side == 1 ? 0 : 1;
+  const int64_t n_other = c->n[other];
+  for (int64_t i = 0; i < n_rows; ++i)
+    if (row_ptr[i + 1] < row_ptr[i])
+      return fail(c, FRECSYS_ERR_INVALID, "frecsys_load_csr: row_ptr not monotone");
+  for (int64_t k = 0; k < nnz; ++k)
+    if (col[k] < 0 || col[k] >= n_other)  // assert(cp < item_embeddings.rows()), ials.h:116
+      return fail(c, FRECSYS_ERR_INVALID,
+                  "frecsys_load_csr: column id " + std::to_string(col[k]) + " out of range");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->rp[side]) HIP_TRY(c, hipFree(c->rp[side]));
+  if (c->col[side]) HIP_TRY(c, hipFree(c->col[side]));
+  c->rp[side] = nullptr;
+  c->col[side] = nullptr;
+  HIP_TRY(c, hipMalloc((void**)&c->rp[side], sizeof(int64_t) * (n_rows + 1)));
+  HIP_TRY(c, hipMalloc((void**)&c->col[side], sizeof(int32_t) * std::max<int64_t>(nnz, 1)));
+  HIP_TRY(c, hipMemcpyAsync(c->rp[side], row_ptr, sizeof(int64_t) * (n_rows + 1),
+                            hipMemcpyHostToDevice, c->stream));
+  if (nnz)
+    HIP_TRY(c, hipMemcpyAsync(c->col[side], col, sizeof(int32_t) * nnz, hipMemcpyHostToDevice,
+                              c->stream));
+  c->nnz[side] = nnz;
+  if (side == 2) {
+    c->n[2] = n_rows;
+    if (c->emb[2]) HIP_TRY(c, hipFree(c->emb[2]));
+    c->emb[2] = nullptr;
+    HIP_TRY(c, hipMalloc((void**)&c->emb[2],
+                         sizeof(float) * std::max<int64_t>(n_rows, 1) * c->Dp));
+    HIP_TRY(c, hipMemsetAsync(c->emb[2], 0, sizeof(float) * std::max<int64_t>(n_rows, 1) * c->Dp,
+                              c->stream));
+  } else {
+    c->host_rp[side].assign(row_ptr, row_ptr + n_rows + 1);
+    refresh_bounds(c, side);
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_set_embeddings(frecsys_ctx* c, int32_t side, const float* host, int64_t ld) {
+  if (!c || !valid_side(side) || !host || ld < c->dim)
+    return fail(c, FRECSYS_ERR_INVALID, "frecsys_set_embeddings: bad arguments");
+  if (!c->emb[side]) return fail(c, FRECSYS_ERR_INVALID, "side has no embeddings yet");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int64_t rows = c->n[side];
+  HIP_TRY(c, hipMemsetAsync(c->emb[side], 0, sizeof(float) * std::max<int64_t>(rows, 1) * c->Dp,
+                            c->stream));
+  if (rows)
+    HIP_TRY(c, hipMemcpy2DAsync(c->emb[side], sizeof(float) * c->Dp, host, sizeof(float) * ld,
+                                sizeof(float) * c->dim, rows, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_get_embeddings(frecsys_ctx* c, int32_t side, float* host, int64_t ld) {
+  if (!c || !valid_side(side) || !host || ld < c->dim)
+    return fail(c, FRECSYS_ERR_INVALID, "frecsys_get_embeddings: bad arguments");
+  if (!c->emb[side]) return fail(c, FRECSYS_ERR_INVALID, "side has no embeddings yet");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int64_t rows = c->n[side];
+  if (rows)
+    HIP_TRY(c, hipMemcpy2DAsync(host, sizeof(float) * ld, c->emb[side], sizeof(float) * c->Dp,
+                                sizeof(float) * c->dim, rows, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_init_embeddings(frecsys_ctx* c, uint32_t seed, float stdev) {
+  if (!c) return fail(c, FRECSYS_ERR_INVALID, "null ctx");
+  // ials.h:47-51: adjusted_stdev = stdev / sqrt(embedding_dim); one
+  // generator, a new distribution per matrix (recommender.h:61-67).
+  std::mt19937 gen{seed};
+  const float adjusted = (float)((double)stdev / std::sqrt((double)c->dim));
+  for (int s = 0; s < 2; ++s) {
+    NormalF d;
+    std::vector<float> h((size_t)c->n[s] * c->dim);
+    for (auto& v : h) v = d(gen, 0.0f, adjusted);
+    if (c->n[s]) {
+      int rc = frecsys_set_embeddings(c, s, h.data(), c->dim);
+      if (rc) return rc;
+    }
+  }
+  return FRECSYS_OK;
+}
+
+int frecsys_snapshot(frecsys_ctx* c, int32_t side) {
+  if (!c || side < 0 || side > 1) return fail(c, FRECSYS_ERR_INVALID, "snapshot: bad side");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t bytes = sizeof(float) * std::max<int64_t>(c->n[side], 1) * c->Dp;
+  if (!c->snap[side]) HIP_TRY(c, hipMalloc((void**)&c->snap[side], bytes));
+  HIP_TRY(c, hipMemcpyAsync(c->snap[side], c->emb[side], bytes, hipMemcpyDeviceToDevice,
+                            c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_gramian(frecsys_ctx* c, int32_t side, const float* weights, int32_t from_snapshot,
+                    float* host_out) {
+  if (!c || side < 0 || side > 1) return fail(c, FRECSYS_ERR_INVALID, "gramian: bad side");
+  if (from_snapshot && !c->snap[side])
+    return fail(c, FRECSYS_ERR_INVALID, "gramian: no snapshot taken");
+  HIP_TRY(c, hipSetDevice(c->device));
+  int64_t lo, hi;
+  shard(c, side, &lo, &hi);
+  const int64_t rows = hi - lo;
+  int rc;
+  const float* dw = nullptr;
+  if (weights) {
+    rc = upload(c, &c->d_gram_w, &c->cap_gram_w, weights, (size_t)c->n[side]);
+    if (rc) return rc;
+    dw = c->d_gram_w;
+  }
+  rc = ensure(c, &c->d_partials, &c->cap_partials, gram_workspace_floats(c->Dp, rows));
+  if (rc) return rc;
+  GramArgs g;
+  g.X = from_snapshot ? c->snap[side] : c->emb[side];
+  g.row0 = lo;
+  g.n = rows;
+  g.w = dw;
+  g.partials = c->d_partials;
+  g.G = c->gram[side];
+  {
+    ScopedTimer t(c, "gramian");
+    HIP_TRY(c, launch_gramian(c->Dp, g, c->stream));
+    t.stop();
+  }
+  if (c->world > 1) {
+    ScopedTimer t(c, "allreduce");
+    NCCL_TRY(c, ncclAllReduce(c->gram[side], c->gram[side], (size_t)c->Dp * c->Dp, ncclFloat,
+                              ncclSum, c->comm, c->stream));
+    t.stop();
+  }
+  if (host_out)
+    HIP_TRY(c, hipMemcpy2DAsync(host_out, sizeof(float) * c->dim, c->gram[side],
+                                sizeof(float) * c->Dp, sizeof(float) * c->dim, c->dim,
+                                hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_solve_side(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p) {
+  if (!c || !valid_side(side) || !p) return fail(c, FRECSYS_ERR_INVALID, "solve: bad arguments");
+  if (!c->rp[side]) return fail(c, FRECSYS_ERR_INVALID, "solve: no CSR loaded for side");
+  const int kind = p->kind;
+  if (kind < FRECSYS_KIND_IALS || kind > FRECSYS_KIND_CVAR_GRAD_V)
+    return fail(c, FRECSYS_ERR_INVALID, "solve: bad kind");
+  const bool vkind = kind == FRECSYS_KIND_WEIGHTED_V || kind == FRECSYS_KIND_CVAR_GRAD_V;
+  const bool ukind = kind == FRECSYS_KIND_WEIGHTED_U || kind == FRECSYS_KIND_CVAR_GRAD_U;
+  const bool grad = kind == FRECSYS_KIND_CVAR_GRAD_U || kind == FRECSYS_KIND_CVAR_GRAD_V;
+  if (vkind && (!p->entity_reg || !p->other_weight))
+    return fail(c, FRECSYS_ERR_INVALID, "solve: V kinds need entity_reg and other_weight");
+  if (grad && side == 2) return fail(c, FRECSYS_ERR_INVALID, "solve: CVaR step on EVAL side");
+  const int other = side == 1 ? 0 : 1;
+  if (p->from_snapshot && !c->snap[other])
+    return fail(c, FRECSYS_ERR_INVALID, "solve: from_snapshot without a snapshot");
+  HIP_TRY(c, hipSetDevice(c->device));
+  int rc;
+  if (ukind && p->entity_weight) {
+    rc = upload(c, &c->d_entity_weight, &c->cap_entity_weight, p->entity_weight,
+                (size_t)c->n[side]);
+    if (rc) return rc;
+  }
+  if (vkind) {
+    rc = upload(c, &c->d_entity_reg, &c->cap_entity_reg, p->entity_reg, (size_t)c->n[side]);
+    if (rc) return rc;
+    rc = upload(c, &c->d_other_weight, &c->cap_other_weight, p->other_weight,
+                (size_t)c->n[other]);
+    if (rc) return rc;
+  }
+  int64_t lo, hi;
+  shard(c, side, &lo, &hi);
+  SolveArgs a;
+  a.kind = kind;
+  a.quirk = c->quirks;
+  a.row_ptr = c->rp[side];
+  a.col = c->col[side];
+  a.row_lo = lo;
+  a.n_rows = hi - lo;
+  a.X = p->from_snapshot ? c->snap[other] : c->emb[other];
+  a.n_other = c->n[other];
+  a.G = c->gram[other];
+  a.E = c->emb[side];
+  a.out = c->emb[side];
+  a.reg = p->reg;
+  a.reg_exp = p->reg_exp;
+  a.w = p->unobserved_weight;
+  a.alpha = p->alpha;
+  a.eta = p->stepsize;
+  a.entity_weight = (ukind && p->entity_weight) ? c->d_entity_weight : nullptr;
+  a.entity_reg = vkind ? c->d_entity_reg : nullptr;
+  a.other_weight = vkind ? c->d_other_weight : nullptr;
+  a.fail = c->d_fail;
+  const unsigned long long none = ~0ull;
+  HIP_TRY(c, hipMemcpyAsync(c->d_fail, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
+  {
+    static const char* names[3] = {"solve_user", "solve_item", "solve_eval"};
+    ScopedTimer t(c, names[side]);
+    HIP_TRY(c, launch_solve(c->Dp, a, c->stream));
+    t.stop();
+  }
+  unsigned long long f = none;
+  HIP_TRY(c, hipMemcpyAsync(&f, c->d_fail, sizeof(f), hipMemcpyDeviceToHost, c->stream));
+  if (side < 2 && c->world > 1) {
+    ScopedTimer t(c, "allgather");
+    rc = allgather_rows(c, c->emb[side], side, c->Dp);
+    if (rc) return rc;
+    t.stop();
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (f != none) {
+    c->err_entity = (int64_t)f - 1;
+    return fail(c, FRECSYS_ERR_NOT_SPD,
+                "LLT failed (matrix not SPD) for entity " + std::to_string(c->err_entity));
+  }
+  return FRECSYS_OK;
+}
+
+int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, float* host_out) {
+  if (!c || (side != 0 && side != 2)) return fail(c, FRECSYS_ERR_INVALID, "loss: bad side");
+  if (!c->rp[side]) return fail(c, FRECSYS_ERR_INVALID, "loss: no CSR loaded");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t rows = (size_t)c->n[side];
+  const bool fresh = c->cap_loss < rows || !c->d_loss;
+  int rc = ensure(c, &c->d_loss, &c->cap_loss, rows);
+  if (rc) return rc;
+  if (fresh || side == 2)
+    HIP_TRY(c, hipMemsetAsync(c->d_loss, 0, sizeof(float) * std::max<size_t>(rows, 1), c->stream));
+  int64_t lo, hi;
+  shard(c, side, &lo, &hi);
+  LossArgs a;
+  a.row_ptr = c->rp[side];
+  a.col = c->col[side];
+  a.row_lo = lo;
+  a.n_rows = hi - lo;
+  a.U = c->emb[side];
+  a.V = c->emb[1];
+  a.G = c->gram[1];
+  a.beta = beta;
+  a.half = half;
+  a.out = c->d_loss;
+  {
+    ScopedTimer t(c, "user_loss");
+    HIP_TRY(c, launch_user_loss(c->Dp, a, c->stream));
+    t.stop();
+  }
+  if (host_out) {
+    if (side == 0 && c->world > 1) {
+      rc = allgather_rows(c, c->d_loss, 0, 1);
+      if (rc) return rc;
+    }
+    if (rows)
+      HIP_TRY(c, hipMemcpyAsync(host_out, c->d_loss, sizeof(float) * rows, hipMemcpyDeviceToHost,
+                                c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_synchronize(frecsys_ctx* c) {
+  if (!c) return FRECSYS_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_timing(const frecsys_ctx* c, const char* what, double* total_ms, int64_t* launches) {
+  if (!c || !what) return FRECSYS_ERR_INVALID;
+  auto it = c->timers.find(what);
+  if (total_ms) *total_ms = it == c->timers.end() ? 0.0 : it->second.total_ms;
+  if (launches) *launches = it == c->timers.end() ? 0 : it->second.launches;
+  return FRECSYS_OK;
+}
+
+int frecsys_timing_reset(frecsys_ctx* c) {
+  if (!c) return FRECSYS_ERR_INVALID;
+  c->timers.clear();
+  return FRECSYS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,250 @@
+"""frecsys_hip -- ctypes binding of libfrecsys_hip.so (include/frecsys_hip.h).
+
+Thin host-side plumbing over the C-ABI for the Python harnesses (tests,
+bench.py, __graft_entry__).  The product's own host layer is C++
+(include/frecsys/*.h, tools/run_model.cc); this module adds nothing to the
+compute path: every call goes straight to the HIP library, and importing it
+without the built library raises (there is no CPU fallback).
+
+Sides / kinds mirror the C-ABI (`SIDE_USER`, `KIND_IALS`, ...).  Arrays are
+numpy: CSR row_ptr int64, col int32, embeddings float32 [rows, dim].
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+
+SIDE_USER, SIDE_ITEM, SIDE_EVAL = 0, 1, 2
+KIND_IALS, KIND_WEIGHTED_U, KIND_WEIGHTED_V, KIND_CVAR_GRAD_U, KIND_CVAR_GRAD_V = range(5)
+
+OK = 0
+ERR_INVALID, ERR_HIP, ERR_RCCL, ERR_NOT_SPD, ERR_NAN, ERR_UNSUPPORTED, ERR_NO_DEVICE = range(1, 8)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfrecsys_hip.so")
+
+# Every symbol include/frecsys_hip.h declares (checked by the CPU tests).
+EXPORTS = (
+    "frecsys_device_count", "frecsys_ctx_create", "frecsys_ctx_destroy",
+    "frecsys_last_error", "frecsys_last_error_entity", "frecsys_padded_dim",
+    "frecsys_partition", "frecsys_comm_unique_id", "frecsys_comm_init",
+    "frecsys_shard_range", "frecsys_load_csr", "frecsys_set_embeddings",
+    "frecsys_get_embeddings", "frecsys_init_embeddings", "frecsys_snapshot",
+    "frecsys_gramian", "frecsys_solve_side", "frecsys_user_loss",
+    "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset",
+)
+
+
+class FrecsysError(RuntimeError):
+    def __init__(self, code: int, msg: str, entity: int = -1):
+        super().__init__(f"frecsys error {code}: {msg}")
+        self.code = code
+        self.entity = entity
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("dim", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("parity_quirks", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("n_users", ctypes.c_int64), ("n_items", ctypes.c_int64)]
+
+
+class _SolveParams(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("reg", ctypes.c_float),
+                ("reg_exp", ctypes.c_float), ("unobserved_weight", ctypes.c_float),
+                ("alpha", ctypes.c_float), ("stepsize", ctypes.c_float),
+                ("from_snapshot", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("entity_weight", ctypes.c_void_p), ("entity_reg", ctypes.c_void_p),
+                ("other_weight", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libfrecsys_hip.so; raises if it was not built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FrecsysError(ERR_INVALID, f"{path} missing: run __graft_entry__.build() / make")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    P, I32, I64, F = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float
+    sig = {
+        "frecsys_device_count": (ctypes.c_int, [P]),
+        "frecsys_ctx_create": (ctypes.c_int, [P, P]),
+        "frecsys_ctx_destroy": (None, [P]),
+        "frecsys_last_error": (ctypes.c_char_p, [P]),
+        "frecsys_last_error_entity": (I64, [P]),
+        "frecsys_padded_dim": (I32, [I32]),
+        "frecsys_partition": (ctypes.c_int, [I64, P, I32, P]),
+        "frecsys_comm_unique_id": (ctypes.c_int, [P]),
+        "frecsys_comm_init": (ctypes.c_int, [P, I32, I32, P]),
+        "frecsys_shard_range": (ctypes.c_int, [P, I32, P, P]),
+        "frecsys_load_csr": (ctypes.c_int, [P, I32, I64, P, P]),
+        "frecsys_set_embeddings": (ctypes.c_int, [P, I32, P, I64]),
+        "frecsys_get_embeddings": (ctypes.c_int, [P, I32, P, I64]),
+        "frecsys_init_embeddings": (ctypes.c_int, [P, ctypes.c_uint32, F]),
+        "frecsys_snapshot": (ctypes.c_int, [P, I32]),
+        "frecsys_gramian": (ctypes.c_int, [P, I32, P, I32, P]),
+        "frecsys_solve_side": (ctypes.c_int, [P, I32, P]),
+        "frecsys_user_loss": (ctypes.c_int, [P, I32, F, I32, P]),
+        "frecsys_synchronize": (ctypes.c_int, [P]),
+        "frecsys_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, P]),
+        "frecsys_timing_reset": (ctypes.c_int, [P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = ctypes.c_int32(0)
+    lib.frecsys_device_count(ctypes.byref(n))
+    return int(n.value)
+
+
+def padded_dim(dim: int) -> int:
+    return int(load_library().frecsys_padded_dim(dim))
+
+
+def partition(row_ptr: np.ndarray, nparts: int) -> np.ndarray:
+    """nnz-balanced contiguous split (host-only; no GPU needed)."""
+    lib = load_library()
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+    out = np.zeros(nparts + 1, dtype=np.int64)
+    rc = lib.frecsys_partition(len(rp) - 1, _ptr(rp), nparts, _ptr(out))
+    if rc:
+        raise FrecsysError(rc, lib.frecsys_last_error(None).decode())
+    return out
+
+
+def unique_id() -> bytes:
+    lib = load_library()
+    buf = (ctypes.c_uint8 * 128)()
+    rc = lib.frecsys_comm_unique_id(buf)
+    if rc:
+        raise FrecsysError(rc, lib.frecsys_last_error(None).decode())
+    return bytes(buf)
+
+
+class Context:
+    """One device context (one GPU).  See include/frecsys_hip.h."""
+
+    def __init__(self, dim: int, n_users: int, n_items: int, device: int = -1,
+                 parity_quirks: bool = True):
+        self.lib = load_library()
+        cfg = _Config(dim, device, 1 if parity_quirks else 0, 0, n_users, n_items)
+        h = ctypes.c_void_p()
+        rc = self.lib.frecsys_ctx_create(ctypes.byref(cfg), ctypes.byref(h))
+        if rc:
+            raise FrecsysError(rc, self.lib.frecsys_last_error(None).decode())
+        self.h = h
+        self.dim = dim
+        self.n = {SIDE_USER: n_users, SIDE_ITEM: n_items, SIDE_EVAL: 0}
+
+    # -- helpers --
+    def _check(self, rc: int):
+        if rc:
+            ent = int(self.lib.frecsys_last_error_entity(self.h))
+            raise FrecsysError(rc, self.lib.frecsys_last_error(self.h).decode(), ent)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.frecsys_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- comm --
+    def comm_init(self, world: int, rank: int, uid: bytes):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.lib.frecsys_comm_init(self.h, world, rank, buf))
+
+    def shard_range(self, side: int) -> Tuple[int, int]:
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.frecsys_shard_range(self.h, side, ctypes.byref(lo), ctypes.byref(hi)))
+        return int(lo.value), int(hi.value)
+
+    # -- data --
+    def load_csr(self, side: int, row_ptr: np.ndarray, col: np.ndarray):
+        rp = np.ascontiguousarray(row_ptr, dtype=np.int64)
+        cl = np.ascontiguousarray(col, dtype=np.int32)
+        self._check(self.lib.frecsys_load_csr(self.h, side, len(rp) - 1, _ptr(rp), _ptr(cl)))
+        if side == SIDE_EVAL:
+            self.n[SIDE_EVAL] = len(rp) - 1
+
+    def set_embeddings(self, side: int, emb: np.ndarray):
+        e = np.ascontiguousarray(emb, dtype=np.float32)
+        assert e.shape == (self.n[side], self.dim), (e.shape, self.n[side], self.dim)
+        self._check(self.lib.frecsys_set_embeddings(self.h, side, _ptr(e), self.dim))
+
+    def get_embeddings(self, side: int) -> np.ndarray:
+        out = np.empty((self.n[side], self.dim), dtype=np.float32)
+        self._check(self.lib.frecsys_get_embeddings(self.h, side, _ptr(out), self.dim))
+        return out
+
+    def init_embeddings(self, seed: int, stdev: float):
+        self._check(self.lib.frecsys_init_embeddings(self.h, seed, stdev))
+
+    def snapshot(self, side: int):
+        self._check(self.lib.frecsys_snapshot(self.h, side))
+
+    # -- compute --
+    def gramian(self, side: int, weights: Optional[np.ndarray] = None,
+                from_snapshot: bool = False, fetch: bool = True) -> Optional[np.ndarray]:
+        w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float32)
+        out = np.empty((self.dim, self.dim), dtype=np.float32) if fetch else None
+        self._check(self.lib.frecsys_gramian(self.h, side, _ptr(w), 1 if from_snapshot else 0,
+                                             _ptr(out)))
+        return out
+
+    def solve_side(self, side: int, kind: int, reg: float, unobserved_weight: float,
+                   reg_exp: float = 1.0, alpha: float = 0.0, stepsize: float = 0.0,
+                   from_snapshot: bool = False, entity_weight=None, entity_reg=None,
+                   other_weight=None):
+        ew = None if entity_weight is None else np.ascontiguousarray(entity_weight, np.float32)
+        er = None if entity_reg is None else np.ascontiguousarray(entity_reg, np.float32)
+        ow = None if other_weight is None else np.ascontiguousarray(other_weight, np.float32)
+        p = _SolveParams(kind, reg, reg_exp, unobserved_weight, alpha, stepsize,
+                         1 if from_snapshot else 0, 0,
+                         None if ew is None else ew.ctypes.data,
+                         None if er is None else er.ctypes.data,
+                         None if ow is None else ow.ctypes.data)
+        self._check(self.lib.frecsys_solve_side(self.h, side, ctypes.byref(p)))
+
+    def user_loss(self, side: int, beta: float, half: bool, fetch: bool = True):
+        out = np.zeros(self.n[side], dtype=np.float32) if fetch else None
+        self._check(self.lib.frecsys_user_loss(self.h, side, beta, 1 if half else 0, _ptr(out)))
+        return out
+
+    def synchronize(self):
+        self._check(self.lib.frecsys_synchronize(self.h))
+
+    def timing(self, what: str) -> Tuple[float, int]:
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        self._check(self.lib.frecsys_timing(self.h, what.encode(), ctypes.byref(ms),
+                                            ctypes.byref(n)))
+        return float(ms.value), int(n.value)
+
+    def timing_reset(self):
+        self._check(self.lib.frecsys_timing_reset(self.h))

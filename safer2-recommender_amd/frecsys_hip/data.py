@@ -1,0 +1,129 @@
+"""Interaction data as CSR for both orientations (host side, numpy).
+
+`Dataset` mirrors frecsys::Dataset (dataset.h:71-99): a `uid,sid` CSV whose
+header line is always skipped (dataset.h:80 -- the reference skips it inside
+an assert, which its build keeps live), each entity's history in FILE ORDER
+(dataset.h:87-88), max_user / max_item / num_tuples.  Instead of
+unordered_map<int, vector<pair<int,int>>> it keeps CSR arrays:
+  by_user: row_ptr[n_users+1] (int64), col[nnz] (int32 item ids)
+  by_item: row_ptr[n_items+1] (int64), col[nnz] (int32 user ids)
+The rating index of the reference's pairs is the file position; by_item rows
+list users in file order (a stable sort of the user-major file by item).
+
+`synthetic` builds the deterministic ML-20M / MSD-shaped inputs of
+BASELINE.md section 4 directly in CSR (no CSV).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+
+def _csr_from_pairs(rows: np.ndarray, cols: np.ndarray, n_rows: int):
+    order = np.argsort(rows, kind="stable")  # keeps file order inside a row
+    counts = np.bincount(rows, minlength=n_rows)
+    row_ptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(counts, out=row_ptr[1:])
+    return row_ptr, np.ascontiguousarray(cols[order], dtype=np.int32)
+
+
+@dataclass
+class Dataset:
+    users: np.ndarray  # file-order user id per tuple
+    items: np.ndarray  # file-order item id per tuple
+    max_user: int
+    max_item: int
+
+    @classmethod
+    def from_csv(cls, path: str) -> "Dataset":
+        data = np.loadtxt(path, delimiter=",", skiprows=1, dtype=np.int64, ndmin=2)
+        if data.size == 0:
+            return cls(np.zeros(0, np.int64), np.zeros(0, np.int64), -1, -1)
+        u, i = data[:, 0], data[:, 1]
+        return cls(u, i, int(u.max()), int(i.max()))
+
+    @property
+    def num_tuples(self) -> int:
+        return int(len(self.users))
+
+    def by_user(self, n_users: int | None = None):
+        n = self.max_user + 1 if n_users is None else n_users
+        return _csr_from_pairs(self.users, self.items, n)
+
+    def by_item(self, n_items: int | None = None):
+        n = self.max_item + 1 if n_items is None else n_items
+        return _csr_from_pairs(self.items, self.users, n)
+
+    def compact_users(self):
+        """Rows = distinct users (sorted by id) -> (user_ids, row_ptr, col).
+        EvaluateDataset's user_to_ind compaction (ials.h:151-166)."""
+        ids, inv = np.unique(self.users, return_inverse=True)
+        rp, col = _csr_from_pairs(inv.astype(np.int64), self.items, len(ids))
+        return ids, rp, col
+
+
+@dataclass
+class SynthShape:
+    n_users: int
+    n_items: int
+    nnz: int
+    min_uc: int = 5
+    zipf_s: float = 1.0
+    sigma: float = 1.0
+
+
+SHAPES = {
+    # BASELINE.md section 4 / SURVEY 8(d)
+    "ml20m": SynthShape(116_677, 20_108, 8_540_000, min_uc=5),
+    "msd": SynthShape(471_355, 41_140, 27_700_000, min_uc=20),
+    "2m500k": SynthShape(2_000_000, 500_000, 100_000_000, min_uc=5),
+    "tiny": SynthShape(3_000, 1_500, 90_000, min_uc=5),
+}
+
+
+def synthetic(shape: SynthShape, seed: int = 98765):
+    """Deterministic synthetic interactions: Zipf(s) item
+    popularity over a seeded permutation, lognormal user history lengths
+    clipped at min_uc and rescaled to the target nnz, items per user drawn
+    by popularity without repeats, every item given >= 1 interaction, rows in
+    user-block order.  Returns (by_user_ptr, by_user_col, by_item_ptr,
+    by_item_col)."""
+    rng = np.random.default_rng(seed)
+    nu, ni = shape.n_users, shape.n_items
+    pop = 1.0 / np.arange(1, ni + 1, dtype=np.float64) ** shape.zipf_s
+    pop = pop[rng.permutation(ni)]
+    cdf = np.cumsum(pop)
+    cdf /= cdf[-1]
+    lens = rng.lognormal(0.0, shape.sigma, nu)
+    lens = lens / lens.sum() * shape.nnz
+    lens = np.clip(np.round(lens), shape.min_uc, ni // 2).astype(np.int64)
+    # oversample 25% then drop repeats inside each user, trim to the target
+    draw = (lens * 1.25 + 4).astype(np.int64)
+    tot = int(draw.sum())
+    users = np.repeat(np.arange(nu, dtype=np.int64), draw)
+    items = np.searchsorted(cdf, rng.random(tot)).astype(np.int64)
+    np.minimum(items, ni - 1, out=items)
+    key = users * ni + items
+    _, first = np.unique(key, return_index=True)
+    first.sort()
+    users, items = users[first], items[first]
+    # rank inside the user (positions kept in draw order), keep < lens[u]
+    starts = np.zeros(nu + 1, dtype=np.int64)
+    np.cumsum(np.bincount(users, minlength=nu), out=starts[1:])
+    rank = np.arange(len(users), dtype=np.int64) - starts[users]
+    keep = rank < lens[users]
+    users, items = users[keep], items[keep]
+    # every item at least once: give each missing item to a random user
+    seen = np.zeros(ni, dtype=bool)
+    seen[items] = True
+    missing = np.nonzero(~seen)[0]
+    if len(missing):
+        extra_u = rng.integers(0, nu, len(missing))
+        users = np.concatenate([users, extra_u])
+        items = np.concatenate([items, missing])
+        order = np.argsort(users, kind="stable")
+        users, items = users[order], items[order]
+    up, uc = _csr_from_pairs(users, items, nu)
+    ip, ic = _csr_from_pairs(items, users, ni)
+    return up, uc, ip, ic

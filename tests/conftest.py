@@ -1,0 +1,82 @@
+"""Shared test setup.
+
+Markers: `gpu` -- needs a visible MI355X and the built libfrecsys_hip.so.
+Everything else runs on the CPU (oracle checks, host logic, ABI exports,
+gloo multi-process tests).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "safer2-recommender_amd")
+for p in (os.path.join(ROOT, "oracle"), PKG, os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+ML1M = os.path.join(GOLDEN, "ml-1m")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X) and the HIP library")
+
+
+@pytest.fixture(scope="session")
+def ml1m():
+    from frecsys_hip.data import Dataset
+    tr = Dataset.from_csv(os.path.join(ML1M, "train.csv"))
+    vt = Dataset.from_csv(os.path.join(ML1M, "validation_tr.csv"))
+    ve = Dataset.from_csv(os.path.join(ML1M, "validation_te.csv"))
+    return tr, vt, ve
+
+
+def make_quirk_data(seed=7, n_users=700, n_items=400, hot_items=(3, 11, 57, 200, 399),
+                    hot_frac=(0.40, 0.19, 0.29, 0.186, 0.5), idle_user=5, idle_item=9):
+    """Small interaction set that hits the reference's edge cases: user
+    histories of length 1 / 5 / 128 / 129 / 200 / 300, item histories above
+    128 with a non-zero remainder mod 128 (ProjectV tail quirk), exactly 256,
+    one idle user and one idle item (rows with no history).  Returns
+    (n_users, n_items, up, uc, ip, ic)."""
+    rng = np.random.default_rng(seed)
+    fixed = {0: 1, 1: 5, 2: 128, 3: 129, 4: 200, 6: 300}
+    users, items = [], []
+    hot = np.array(hot_items)
+    for u in range(n_users):
+        if u == idle_user:
+            continue
+        h = fixed.get(u, int(np.clip(rng.lognormal(3.0, 0.7), 2, 150)))
+        chosen = set()
+        for it, fr in zip(hot, hot_frac):
+            if rng.random() < fr and len(chosen) < h:
+                chosen.add(int(it))
+        pool = rng.permutation(n_items)
+        for it in pool:
+            if len(chosen) >= h:
+                break
+            if it != idle_item:
+                chosen.add(int(it))
+        lst = list(chosen)
+        rng.shuffle(lst)
+        users += [u] * len(lst)
+        items += lst
+    users = np.array(users, np.int64)
+    items = np.array(items, np.int64)
+    from frecsys_hip.data import _csr_from_pairs
+    up, uc = _csr_from_pairs(users, items, n_users)
+    ip, ic = _csr_from_pairs(items, users, n_items)
+    return n_users, n_items, up, uc, ip, ic
+
+
+@pytest.fixture(scope="session")
+def quirk_data():
+    return make_quirk_data()
+
+
+def rel_rows(x, ref):
+    """Per-row relative error ||x - ref|| / ||ref|| (rows with ref == 0 use abs)."""
+    num = np.linalg.norm(x.astype(np.float64) - ref.astype(np.float64), axis=1)
+    den = np.linalg.norm(ref.astype(np.float64), axis=1)
+    return np.where(den > 0, num / np.maximum(den, 1e-30), num)
