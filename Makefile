@@ -19,7 +19,7 @@ HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h include/frecsys_hip.h
 
 .PHONY: all lib oracle run_model clean
-all: lib oracle run_model
+all: lib oracle
 lib: $(LIB)
 oracle: $(ORACLE)
 run_model: $(RUNMODEL)

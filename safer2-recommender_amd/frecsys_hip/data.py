@@ -70,6 +70,7 @@ class SynthShape:
     nnz: int
     min_uc: int = 5
     zipf_s: float = 1.0
+    zipf_q: float = 10.0
     sigma: float = 1.0
 
 
@@ -83,23 +84,25 @@ SHAPES = {
 
 
 def synthetic(shape: SynthShape, seed: int = 98765):
-    """Deterministic synthetic interactions: Zipf(s) item
-    popularity over a seeded permutation, lognormal user history lengths
+    """Deterministic synthetic interactions: Zipf-Mandelbrot
+    item popularity 1/(rank+q)^s (s=1, q=10: the most popular item reaches
+    ~55% of users, close to ML-20M's head; plain Zipf puts one item in >99%
+    of histories) over a seeded permutation, lognormal user history lengths
     clipped at min_uc and rescaled to the target nnz, items per user drawn
     by popularity without repeats, every item given >= 1 interaction, rows in
     user-block order.  Returns (by_user_ptr, by_user_col, by_item_ptr,
     by_item_col)."""
     rng = np.random.default_rng(seed)
     nu, ni = shape.n_users, shape.n_items
-    pop = 1.0 / np.arange(1, ni + 1, dtype=np.float64) ** shape.zipf_s
+    pop = 1.0 / (np.arange(1, ni + 1, dtype=np.float64) + shape.zipf_q) ** shape.zipf_s
     pop = pop[rng.permutation(ni)]
     cdf = np.cumsum(pop)
     cdf /= cdf[-1]
     lens = rng.lognormal(0.0, shape.sigma, nu)
     lens = lens / lens.sum() * shape.nnz
     lens = np.clip(np.round(lens), shape.min_uc, ni // 2).astype(np.int64)
-    # oversample 25% then drop repeats inside each user, trim to the target
-    draw = (lens * 1.25 + 4).astype(np.int64)
+    # oversample then drop repeats inside each user, trim to the target
+    draw = (lens * 1.6 + 8).astype(np.int64)
     tot = int(draw.sum())
     users = np.repeat(np.arange(nu, dtype=np.int64), draw)
     items = np.searchsorted(cdf, rng.random(tot)).astype(np.int64)

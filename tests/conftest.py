@@ -43,7 +43,7 @@ def make_quirk_data(seed=7, n_users=700, n_items=400, hot_items=(3, 11, 57, 200,
     rng = np.random.default_rng(seed)
     fixed = {0: 1, 1: 5, 2: 128, 3: 129, 4: 200, 6: 300}
     users, items = [], []
-    hot = np.array(hot_items)
+    hot = np.array(hot_items) % n_items
     for u in range(n_users):
         if u == idle_user:
             continue

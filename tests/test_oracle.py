@@ -1,0 +1,207 @@
+"""Pin the CPU oracle (oracle/frecsys_oracle.c) before trusting it:
+
+1. against the reference's own known-answer tests on its own fixture
+   (tests/ml-1m, copied to tests/golden/ml-1m): NDCG@20 >= 0.2 after the
+   reference's epochs/hyper-parameters (ials_test.cc:17-45,
+   erm_mf_test.cc:17-45, cvar_mf_test.cc:17-46, safer2_test.cc:17-99) and the
+   SAFER2 mean dual weight within alpha +- 0.02 after every epoch
+   (safer2_test.cc:135, 183, 230; the SNR variant is not restated);
+2. against an independent float64 numpy restatement (tests/numpy_ref.py);
+3. against libstdc++'s own std::mt19937 / std::normal_distribution<float>
+   (a tiny C++ program compiled with g++ at test time).
+Element-wise agreement with the reference binary itself is unpinned: the
+reference needs Eigen/glog/bazel, none of which exist in this image.
+"""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import numpy_ref as R
+import oracle as O
+from conftest import make_quirk_data
+
+K_LIST = (5, 10, 20, 50, 100)
+
+
+def test_mt19937_known_answer():
+    # C++ [rand.predef]: the 10000th output of a default-seeded mt19937 is 4123659995
+    import ctypes
+    st = (ctypes.c_uint32 * 625)()
+    O.lib().oracle_mt_seed(st, 5489)
+    v = None
+    for _ in range(10000):
+        v = O.lib().oracle_mt_next(st)
+    assert v == 4123659995
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ missing")
+def test_init_matches_libstdcxx(tmp_path):
+    src = tmp_path / "gen.cc"
+    src.write_text(r'''
+#include <cmath>
+#include <cstdio>
+#include <random>
+int main() {
+  int dim = 7; long nu = 5, ni = 3;
+  std::mt19937 gen{4242u};
+  float s = 0.1 / sqrt(dim);
+  for (int m = 0; m < 2; ++m) {
+    std::normal_distribution<float> d(0, s);
+    long n = (m == 0 ? nu : ni) * dim;
+    for (long i = 0; i < n; ++i) printf("%.9g\n", d(gen));
+  }
+}''')
+    exe = tmp_path / "gen"
+    subprocess.run(["g++", "-O2", "-o", str(exe), str(src)], check=True)
+    ref = np.array([float(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                     check=True).stdout.split()], np.float32)
+    U, V = O.init_embeddings(4242, 0.1, 7, 5, 3)
+    np.testing.assert_array_equal(np.concatenate([U.ravel(), V.ravel()]), ref)
+
+
+@pytest.fixture(scope="module")
+def small():
+    nu, ni, up, uc, ip, ic = make_quirk_data(seed=11, n_users=400, n_items=300)
+    return nu, ni, up, uc, ip, ic
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+@pytest.mark.parametrize("dim", [4, 8, 33])
+def test_projections_vs_numpy(small, dim):
+    nu, ni, up, uc, ip, ic = small
+    U, V = O.init_embeddings(3, 0.1, dim, nu, ni)
+    Gv, Gu = O.gramian(V), O.gramian(U)
+    np.testing.assert_allclose(Gv, V.astype(np.float64).T @ V, rtol=1e-5, atol=1e-7)
+    om = (0.1 + np.random.default_rng(1).random(nu)).astype(np.float32)
+    hu = np.diff(up).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        nuw = (om / hu).astype(np.float32)
+    Ui, _ = O.step(up, uc, V, Gv, 0, 0.003, 0.1)
+    Uu, _ = O.step(up, uc, V, Gv, 1, 0.004, 0.004, entity_weight=om)
+    er = np.linspace(0.5, 2.0, ni).astype(np.float32)
+    Vv, _ = O.step(ip, ic, U, Gu, 2, 0.004, 0.004, alpha=0.3, entity_reg=er, other_weight=nuw)
+    Uc, _ = O.step(up, uc, V, Gv, 3, 0.002, 0.008, stepsize=0.4, entity_weight=om, E=U)
+    Vc, _ = O.step(ip, ic, U, Gu, 4, 0.002, 0.008, alpha=0.3, stepsize=0.4, entity_reg=er,
+                   other_weight=nuw, E=V)
+    for u in range(nu):
+        hist = uc[up[u]:up[u + 1]]
+        if len(hist) == 0:
+            continue
+        lam_i = 0.003 * (len(hist) + 0.1 * ni)
+        assert _rel(Ui[u], R.ials(hist, V, Gv, lam_i, 0.1)) < 1e-4
+        lam_u = 0.004 * (1 + 0.004 * ni)
+        assert _rel(Uu[u], R.project_u(hist, V, Gv, lam_u, 0.004, om[u])) < 1e-4
+        lam_c = 0.002 * (1 + 0.008 * ni)
+        assert _rel(Uc[u], R.cvar_u(hist, U[u], V, Gv, lam_c, 0.008, 0.4, om[u])) < 1e-4
+    for v in range(ni):
+        hist = ic[ip[v]:ip[v + 1]]
+        if len(hist) == 0:
+            continue
+        lam_v = np.float32(0.004) * (er[v] + np.float32(0.3) * np.float32(0.004) * nu)
+        assert _rel(Vv[v], R.project_v(hist, U, Gu, lam_v, 0.004, nuw, True)) < 1e-4
+        lam_cv = np.float32(0.002) * (er[v] + np.float32(0.3) * np.float32(0.008) * nu)
+        assert _rel(Vc[v], R.cvar_v(hist, V[v], U, Gu, lam_cv, 0.008, nuw, 0.4, True)) < 1e-4
+
+
+def test_quirk_matters_in_numpy_and_oracle(small):
+    nu, ni, up, uc, ip, ic = small
+    U, V = O.init_embeddings(3, 0.1, 8, nu, ni)
+    Gu = O.gramian(U)
+    hu = np.diff(up).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        nuw = (0.3 / hu).astype(np.float32)
+    er = np.ones(ni, np.float32)
+    a, _ = O.step(ip, ic, U, Gu, 2, 0.004, 0.004, alpha=0.3, entity_reg=er, other_weight=nuw,
+                  quirk=1)
+    b, _ = O.step(ip, ic, U, Gu, 2, 0.004, 0.004, alpha=0.3, entity_reg=er, other_weight=nuw,
+                  quirk=0)
+    h = np.diff(ip)
+    aff = (h > 128) & (h % 128 != 0)
+    assert aff.any()
+    assert np.all(np.abs(a - b).max(1)[aff] > 0)
+    np.testing.assert_array_equal(a[~aff], b[~aff])
+
+
+def test_user_loss_vs_numpy(small):
+    nu, ni, up, uc, ip, ic = small
+    U, V = O.init_embeddings(5, 0.3, 16, nu, ni)
+    G = O.gramian(V)
+    for half in (False, True):
+        lo = O.user_loss(up, uc, U, V, G, 0.05, half)
+        for u in range(nu):
+            hist = uc[up[u]:up[u + 1]]
+            if len(hist):
+                assert abs(lo[u] - R.user_loss(hist, U[u], V, G, 0.05, half)) <= 1e-5 * abs(lo[u])
+            else:
+                assert lo[u] == 0
+
+
+@pytest.mark.parametrize("epan,bw", [(False, 0.15), (True, 0.7)])
+def test_safer2_scalar_math_vs_numpy(epan, bw):
+    rng = np.random.default_rng(2)
+    losses = (0.2 + 0.3 * rng.random(500)).astype(np.float32)
+    for xi in (0.1, 0.3, 0.45):
+        for l in losses[:20]:
+            assert abs(O.safer2_weight(float(l), xi, bw, epan) -
+                       R.safer2_weight(float(l), xi, bw, epan)) < 2e-6
+    x_o = O.safer2_xi(losses, float(losses.mean()), 5, 0.3, bw, epan)
+    x_r = R.safer2_xi(losses.astype(np.float64), float(losses.mean()), 5, 0.3, bw, epan)
+    assert abs(x_o - x_r) < 1e-4 * max(1.0, abs(x_r))
+
+
+def test_cvar_exact_quantile():
+    l = np.array([0.5, 0.1, 0.9, 0.3, 0.7, 0.2, 0.8, 0.4, 0.6, 0.0], np.float32)
+    # k = floor(10 * 0.3) = 3 -> 4th largest
+    assert O.cvar_xi(l, 0.3) == pytest.approx(0.6)
+
+
+def _run_gate(ml1m, model, epochs, dim=8, **kw):
+    tr, vt, ve = ml1m
+    nu, ni = tr.max_user + 1, tr.max_item + 1
+    up, uc = tr.by_user()
+    ip, ic = tr.by_item()
+    ids, ep, ec = vt.compact_users()
+    ids2, gp, gc = ve.compact_users()
+    assert np.array_equal(ids, ids2)
+    m = O.Model(model, dim, nu, ni, seed=1, **kw)
+    m.set_data(up, uc, ip, ic)
+    m.initialize()
+    weights = []
+    for _ in range(epochs):
+        assert m.train() == 0
+        weights.append(float(m.state()[1].mean()))
+    Ue, rc = m.fold_in(ep, ec)
+    assert rc == 0
+    _, V = m.embeddings()
+    rec, ndcg = O.evaluate(Ue, V, ep, ec, gp, gc, K_LIST)
+    return ndcg.mean(0), weights
+
+
+def test_gate_ials(ml1m):  # ials_test.cc:17-45
+    ndcg, _ = _run_gate(ml1m, O.MODEL_IALS, 10, reg=0.003, w=0.1)
+    assert ndcg[2] >= 0.2
+
+
+def test_gate_erm(ml1m):  # erm_mf_test.cc:17-45
+    ndcg, _ = _run_gate(ml1m, O.MODEL_ERM, 10, reg=0.005, w=0.004)
+    assert ndcg[2] >= 0.2
+
+
+def test_gate_cvar(ml1m):  # cvar_mf_test.cc:17-46
+    ndcg, _ = _run_gate(ml1m, O.MODEL_CVAR, 50, reg=0.002, w=0.008, stepsize=0.4)
+    assert ndcg[2] >= 0.2
+
+
+@pytest.mark.parametrize("epan,bw", [(False, 0.15), (True, 0.7)])
+def test_gate_safer2(ml1m, epan, bw):  # safer2_test.cc:17-32, 66-99, 135, 230
+    ndcg, weights = _run_gate(ml1m, O.MODEL_SAFER2, 10, reg=0.004, w=0.004, bandwidth=bw,
+                              epan=epan, xi_iterations=5, pd_iterations=1)
+    assert ndcg[2] >= 0.2
+    for mw in weights:
+        assert abs(mw - 0.3) <= 0.02
