@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <random>
@@ -63,6 +64,12 @@ struct frecsys_ctx {
   float* d_loss = nullptr;
   size_t cap_loss = 0;
   unsigned long long* d_fail = nullptr;
+  unsigned int* d_counter = nullptr;
+  // per side: the rank's entities in decreasing-history order (LPT queue)
+  QueueRec* d_order[3] = {nullptr, nullptr, nullptr};
+  int64_t order_n[3] = {0, 0, 0};
+  bool order_stale[3] = {true, true, true};
+  std::vector<int64_t> host_rp_eval;
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
   std::string err;
@@ -142,6 +149,43 @@ void shard(const frecsys_ctx* c, int side, int64_t* lo, int64_t* hi) {
   }
   *lo = c->bounds[side][c->rank];
   *hi = c->bounds[side][c->rank + 1];
+}
+
+// Entities of the rank's shard of `side`, longest history first (stable),
+// uploaded as the work queue of the tiled solve kernel (one 16-B record per
+// entity: id, history length, CSR offset).
+int build_order(frecsys_ctx* c, int side) {
+  if (!c->order_stale[side] && c->d_order[side]) return FRECSYS_OK;
+  int64_t lo, hi;
+  shard(c, side, &lo, &hi);
+  const std::vector<int64_t>& rp = side == 2 ? c->host_rp_eval : c->host_rp[side];
+  std::vector<int32_t> ord((size_t)(hi - lo));
+  for (int64_t i = lo; i < hi; ++i) ord[i - lo] = (int32_t)i;
+  std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) {
+    return (rp[x + 1] - rp[x]) > (rp[y + 1] - rp[y]);
+  });
+  std::vector<QueueRec> recs(ord.size());
+  for (size_t i = 0; i < ord.size(); ++i) {
+    const int32_t e = ord[i];
+    recs[i].entity = e;
+    recs[i].h = (int32_t)(rp[e + 1] - rp[e]);
+    recs[i].p0 = rp[e];
+  }
+  if (c->d_order[side]) {
+    hipError_t err = hipFree(c->d_order[side]);
+    (void)err;
+  }
+  c->d_order[side] = nullptr;
+  if (hipMalloc((void**)&c->d_order[side], sizeof(QueueRec) * std::max<size_t>(recs.size(), 1)) !=
+      hipSuccess)
+    return fail(c, FRECSYS_ERR_HIP, "hipMalloc failed (order)");
+  if (!recs.empty() && hipMemcpyAsync(c->d_order[side], recs.data(),
+                                      sizeof(QueueRec) * recs.size(), hipMemcpyHostToDevice,
+                                      c->stream) != hipSuccess)
+    return fail(c, FRECSYS_ERR_HIP, "hipMemcpy failed (order)");
+  c->order_n[side] = (int64_t)recs.size();
+  c->order_stale[side] = false;
+  return FRECSYS_OK;
 }
 
 // Row-range all-gather of a [rows x ld] float matrix (uneven per-rank
@@ -295,7 +339,8 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
     (void)hipMemsetAsync(c->emb[s], 0, sizeof(float) * rows * Dp, c->stream);
     (void)hipMemsetAsync(c->gram[s], 0, sizeof(float) * Dp * Dp, c->stream);
   }
-  if (hipMalloc((void**)&c->d_fail, sizeof(unsigned long long)) != hipSuccess)
+  if (hipMalloc((void**)&c->d_fail, sizeof(unsigned long long)) != hipSuccess ||
+      hipMalloc((void**)&c->d_counter, sizeof(unsigned int)) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_HIP, "hipMalloc failed"));
   c->bounds[0] = {0, c->n[0]};
   c->bounds[1] = {0, c->n[1]};
@@ -323,6 +368,9 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
                    c->d_partials, c->d_loss})
     if (p) (void)hipFree(p);
   if (c->d_fail) (void)hipFree(c->d_fail);
+  if (c->d_counter) (void)hipFree(c->d_counter);
+  for (int s = 0; s < 3; ++s)
+    if (c->d_order[s]) (void)hipFree(c->d_order[s]);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -355,6 +403,7 @@ int frecsys_comm_init(frecsys_ctx* c, int32_t world, int32_t rank, const uint8_t
   }
   refresh_bounds(c, 0);
   refresh_bounds(c, 1);
+  c->order_stale[0] = c->order_stale[1] = true;
   return FRECSYS_OK;
 }
 
@@ -397,7 +446,9 @@ int frecsys_load_csr(frecsys_ctx* c, int32_t side, int64_t n_rows, const int64_t
     HIP_TRY(c, hipMemcpyAsync(c->col[side], col, sizeof(int32_t) * nnz, hipMemcpyHostToDevice,
                               c->stream));
   c->nnz[side] = nnz;
+  c->order_stale[side] = true;
   if (side == 2) {
+    c->host_rp_eval.assign(row_ptr, row_ptr + n_rows + 1);
     c->n[2] = n_rows;
     if (c->emb[2]) HIP_TRY(c, hipFree(c->emb[2]));
     c->emb[2] = nullptr;
@@ -545,8 +596,12 @@ int frecsys_solve_side(frecsys_ctx* c, int32_t side, const frecsys_solve_params*
   }
   int64_t lo, hi;
   shard(c, side, &lo, &hi);
+  rc = build_order(c, side);
+  if (rc) return rc;
   SolveArgs a;
   a.kind = kind;
+  a.order = c->d_order[side];
+  a.counter = c->d_counter;
   a.quirk = c->quirks;
   a.row_ptr = c->rp[side];
   a.col = c->col[side];
@@ -566,6 +621,10 @@ int frecsys_solve_side(frecsys_ctx* c, int32_t side, const frecsys_solve_params*
   a.entity_reg = vkind ? c->d_entity_reg : nullptr;
   a.other_weight = vkind ? c->d_other_weight : nullptr;
   a.fail = c->d_fail;
+  {
+    static const int dbg = getenv("FRECSYS_DEBUG_SKIP") ? atoi(getenv("FRECSYS_DEBUG_SKIP")) : 0;
+    a.debug_skip = dbg;
+  }
   const unsigned long long none = ~0ull;
   HIP_TRY(c, hipMemcpyAsync(c->d_fail, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
   {

@@ -7,14 +7,24 @@
 
 namespace frecsys_hip {
 
+// One entry of the solve queue: entity row, its history length and the
+// offset of its history in the CSR column array (16 B, one load).
+struct QueueRec {
+  int32_t entity;
+  int32_t h;
+  int64_t p0;
+};
+
 // Everything one launch of the per-entity solve needs (device pointers).
 struct SolveArgs {
   int kind;                 // FRECSYS_KIND_*
   int quirk;                // reproduce the ProjectV tail double-count
   const int64_t* row_ptr;   // CSR of the solved side
   const int32_t* col;
-  int64_t row_lo;           // first entity of this launch
+  int64_t row_lo;           // first entity of this launch (small kernel)
   int64_t n_rows;           // entities in this launch
+  const QueueRec* order;    // [n_rows] longest history first (tiled kernel)
+  unsigned int* counter;    // work-queue head, zeroed by the launcher
   const float* X;           // other side's embeddings, ld = Dp
   int64_t n_other;          // rows of the other side (for lambda)
   const float* G;           // Dp x Dp Gramian of the other side
@@ -25,6 +35,7 @@ struct SolveArgs {
   const float* entity_reg;     // [rows of side] item_reg_
   const float* other_weight;   // [rows of other side] nu
   unsigned long long* fail;    // atomicMin(entity + 1) on a non-SPD pivot
+  int debug_skip;              // diagnostic ablation mask (0 in production)
 };
 
 struct GramArgs {

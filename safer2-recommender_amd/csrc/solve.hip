@@ -15,11 +15,14 @@
 //      wave owning a fixed subset of tiles; the epilogue folds in w*G,
 //      lambda and the per-kind scaling and writes A into LDS (XOR-swizzled
 //      tiles, aliasing the staging ring that is dead by then);
-//   3. solve: right-looking blocked Cholesky on the LDS tiles -- a 32x32
-//      diagonal factor (one wave, register rows + readlane broadcasts), a
-//      lane-per-row TRSM of the panel (the right-hand side rides along as
-//      one extra row, so y = L^-1 b comes out of the factorisation), MFMA
-//      trailing updates; then L^T x = y by one wave.
+//   3. solve: right-looking blocked Cholesky on the LDS tiles -- per panel a
+//      32x32 diagonal factor that also yields L_pp^-1 (one wave, see
+//      diag_factor_inv), the panel TRSM as MFMA products with L_pp^-1 (the
+//      right-hand side rides along: y_p = L_pp^-1 b_p), MFMA trailing
+//      updates; then x = L^-T y with one GEMV wave per tile and the stored
+//      inverses.  Workgroup b takes entity order[b]: the rank's entities in
+//      decreasing-history order, so the dispatcher starts the longest first
+//      (LPT scheduling of a skewed workload).
 //   CVaR-MF kinds skip 3 and take one gradient step with the full matrix
 //   whose strict upper triangle lacks the observed term (cvar_mf.h:133).
 //
@@ -70,58 +73,62 @@ __device__ __forceinline__ int64_t virt_pos(int64_t k, int64_t h) {
   return k < h ? k : (h - 128 + (k - h));
 }
 
-// 32x32 diagonal factor by one wave (lane r and r+32 own row r; only lanes
-// < 32 write).  Left-looking over columns: at step k every lane forms
-// t = a[k] - sum_{m<k} a[m] L[k][m] (for lane k that is the pivot); row k of
-// L is read back as LDS broadcasts from the unswizzled copy `ld`, which each
-// lane fills with its own L[r][k] as soon as it is known (LDS operations of
-// one wave complete in issue order).  Writes the factor (upper zeroed) back
-// into the swizzled tile and leaves the row-major copy for the TRSM.
-__device__ __forceinline__ bool diag_factor(float* tile, float* ld, int lane) {
+// ---------------------------------------------------------------------
+// 32x32 diagonal block: Cholesky factor AND its inverse by one wave.
+//
+// Lanes 0..31 own row r of A (becoming row r of L); lanes 32..63 own column
+// j = lane-32 of the identity (becoming column j of L^-1).  Both halves run
+// the same left-looking update at step k,
+//     t = a[k] - sum_{m<k} a[m] * L[k][m],
+// which for a row of A is the Cholesky update and for a column of the
+// identity is forward substitution L x = e_j; then a[k] = t / L[k][k] (lane
+// k itself takes the pivot sqrt).  Row k of L (lane k's registers) reaches
+// every lane by v_readlane -- no LDS round trip on the serial chain; the dot
+// product runs in 4 partial chains.  On return L^-1 (lower, upper zeroed)
+// is in the swizzled tile.
+// ---------------------------------------------------------------------
+__device__ __forceinline__ float rdlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+__device__ __forceinline__ bool diag_factor_inv(float* tile, int lane) {
   const int r = lane & 31;
-  const bool wr = lane < 32;
+  const bool fl = lane < 32;
   float a[32];
 #pragma unroll
-  for (int c = 0; c < 32; ++c) a[c] = tile[sw(r, c)];
+  for (int c = 0; c < 32; ++c) a[c] = fl ? tile[sw(r, c)] : (c == r ? 1.0f : 0.0f);
   bool ok = true;
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
-    float t = a[k];
-#pragma unroll 4
-    for (int m = 0; m < k; ++m) t -= a[m] * ld[k * 32 + m];
-    if (r == k) {
-      ok = t > 0.0f;
-      a[k] = sqrtf(t);
-      if (wr) ld[k * 32 + k] = a[k];
-    }
-    __builtin_amdgcn_wave_barrier();
-    const float d = ld[k * 32 + k];
-    if (r > k) {
-      a[k] = t / d;
-      if (wr) ld[r * 32 + k] = a[k];
-    }
-  }
-  if (wr) {
+    float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
 #pragma unroll
-    for (int c = 0; c < 32; ++c) {
-      const float v = (c <= r) ? a[c] : 0.0f;
-      tile[sw(r, c)] = v;
-      ld[r * 32 + c] = v;
+    for (int m = 0; m < k; m += 4) {
+      p0 += a[m] * rdlane(a[m], k);
+      if (m + 1 < k) p1 += a[m + 1] * rdlane(a[m + 1], k);
+      if (m + 2 < k) p2 += a[m + 2] * rdlane(a[m + 2], k);
+      if (m + 3 < k) p3 += a[m + 3] * rdlane(a[m + 3], k);
     }
+    const float t = a[k] - ((p0 + p1) + (p2 + p3));
+    const float piv = rdlane(t, k);
+    ok = ok && (piv > 0.0f);
+    const float d = sqrtf(piv);
+    const float rd = 1.0f / d;
+    a[k] = (lane == k) ? d : t * rd;
   }
-  // the pivot check lives on lane r == k; fold it over the wave
-  return __all(ok) != 0;
+  if (!fl) {  // column j of L^-1 -> tile element (k, j), k >= j
+    const int j = r;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
+  }
+  return ok;
 }
 
-// Forward substitution x := x L^-T for one row of 32 (L row-major, lower).
-__device__ __forceinline__ void trsm_row(float (&x)[32], const float* L) {
+// One 32x32 MFMA product u = P Q^T of two LDS tiles (P, Q swizzled).
+__device__ __forceinline__ f32x16 tile_pqT(const float* P, const float* Q, int lo, int hi) {
+  f32x16 u = f32x16{0.f};
 #pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    float t = x[k];
-#pragma unroll 4
-    for (int m = 0; m < k; ++m) t -= x[m] * L[k * 32 + m];
-    x[k] = t / L[k * 32 + k];
-  }
+  for (int s = 0; s < 16; ++s) u = mfma32(P[sw(lo, 2 * s + hi)], Q[sw(lo, 2 * s + hi)], u);
+  return u;
 }
 
 template <int T>
@@ -135,7 +142,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
   float* stage = smem;
   float* bvec = smem + C::OFF_B;
   float* xvec = smem + C::OFF_X;
-  float* ldc = smem + C::OFF_LD;
+  float* part = smem + C::OFF_LD;  // back-solve partial sums
   float* ring_sa = smem + C::OFF_SA;
   float* ring_bw = smem + C::OFF_BW;
   int* ring_id = reinterpret_cast<int*>(smem + C::OFF_ID);
@@ -143,18 +150,20 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lo = lane & 31, hi = lane >> 5;
-  const int64_t e = a.row_lo + blockIdx.x;
-  const int64_t p0 = a.row_ptr[e];
-  const int64_t h = a.row_ptr[e + 1] - p0;
-  if (h == 0) return;  // not in by_user / by_item: untouched
   const int kind = a.kind;
   const bool vk = is_v_kind(kind);
+
+  // ---- one entity per workgroup, dispatched in LPT order (longest first) ----
+  const QueueRec rec = a.order[blockIdx.x];
+  const int64_t e = rec.entity;
+  const int64_t h = rec.h;
+  const int64_t p0 = rec.p0;
+  if (h == 0) return;  // not in by_user / by_item: untouched
   int64_t extra = 0;
   if (vk && a.quirk && h > 128 && (h % 128) != 0) extra = 128 - (h % 128);
   const int64_t ntot = h + extra;
   const int nchunks = (int)((ntot + R - 1) / R);
 
-  // ---- ring of history ids + scales, one chunk ahead of the data ----
   auto ring_load = [&](int c, int& id, float& sa, float& bw) {
     const int64_t k = (int64_t)c * R + tid;
     id = -1;
@@ -164,8 +173,8 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
       id = a.col[p0 + virt_pos(k, h)];
       if (vk) {
         const float nu = a.other_weight[id];
-        sa = sqrtf(nu);              // factor col = sqrt(w) * cp_v, safer2.h:192
-        bw = (k < h) ? nu : 0.0f;    // rhs += w * cp_v, safer2.h:190
+        sa = sqrtf(nu);            // factor col = sqrt(w) * cp_v, safer2.h:192
+        bw = (k < h) ? nu : 0.0f;  // rhs += w * cp_v, safer2.h:190
       } else {
         sa = 1.0f;
         bw = 1.0f;
@@ -213,18 +222,24 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     }
   }
   if (is_grad_kind(kind) && tid < Dp) xvec[tid] = a.E[e * Dp + tid];
-  __syncthreads();
-  load_data(0);
-  store_stage(0);
-  __syncthreads();
 
-  // ---- my tiles ----
+  // ---- my tiles; accumulators start from the G part of A ----
+  // (the G reads overlap the history gather that starts below)
+  //  iALS: acc0 = w*G + lam*I        -> A = acc
+  //  U:    acc0 = h*w*G              -> A = acc * (omega/h) + lam*I
+  //  V:    acc0 = w*G                -> A = acc + lam*I
+  //  CVaR: acc0 = 0 (the stale upper triangle needs S and G apart)
+  const float hf = (float)h;
+  const float omega = (is_u_kind(kind) && a.entity_weight) ? a.entity_weight[e] : 1.0f;
+  const float lam =
+      entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other, a.entity_reg, e);
+  const bool grad = is_grad_kind(kind);
+  const float gscale = kind == KIND_IALS ? a.w : (is_u_kind(kind) ? hf * a.w : a.w);
   f32x16 acc[MT];
   int aoff[MT], boff[MT];
   bool valid[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    acc[m] = f32x16{0.f};
     const int t = wave + m * NW;
     valid[m] = t < NT;
     int I = 0;
@@ -232,7 +247,21 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     const int J = t - I * (I + 1) / 2;
     aoff[m] = 32 * I + lo;
     boff[m] = 32 * J + lo;
+    acc[m] = f32x16{0.f};
+    if (valid[m] && !grad) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int gi = 32 * I + acc_row(q, hi), gj = 32 * J + lo;
+        float v = gscale * a.G[gi * Dp + gj];
+        if (kind == KIND_IALS && gi == gj) v += lam;
+        acc[m][q] = v;
+      }
+    }
   }
+  __syncthreads();
+  load_data(0);
+  store_stage(0);
+  __syncthreads();
   float bacc = 0.0f;
 
   for (int c = 0; c < nchunks; ++c) {
@@ -251,7 +280,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
       const float sa = vk ? ring_sa[slot * R + 2 * s + hi] : 1.0f;
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        if (valid[m]) {
+        if (valid[m] && !(a.debug_skip & 1)) {
           float fa = rowp[aoff[m]];
           float fb = rowp[boff[m]];
           if (vk) {
@@ -271,11 +300,8 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     __syncthreads();
   }
 
-  // ---- epilogue: A = f(S, G) into the swizzled LDS tiles ----
-  const float hf = (float)h;
-  const float omega = (is_u_kind(kind) && a.entity_weight) ? a.entity_weight[e] : 1.0f;
-  const float lam = entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other,
-                                  a.entity_reg, e);
+  // ---- epilogue: finish A into the swizzled LDS tiles ----
+  const float us = omega / hf;
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     if (valid[m]) {
@@ -284,21 +310,25 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int i = acc_row(q, hi);
-        const int gi = 32 * I + i, gj = 32 * J + lo;
-        const float g = a.G[(int64_t)gi * Dp + gj];
-        tile[sw(i, lo)] = assemble(kind, acc[m][q], g, gi == gj, a.w, lam, hf, omega);
+        const bool dg = (32 * I + i) == (32 * J + lo);
+        float v = acc[m][q];
+        if (is_u_kind(kind) && !grad) v = v * us + (dg ? lam : 0.0f);
+        else if (vk && !grad) v = v + (dg ? lam : 0.0f);
+        else if (grad) v = assemble(kind, v, a.G[(32 * I + i) * Dp + 32 * J + lo], dg, a.w, lam,
+                                    hf, omega);
+        tile[sw(i, lo)] = v;
       }
     }
   }
   if (tid < Dp) {
     float b = bacc;
-    if (is_u_kind(kind)) b *= (omega / hf);  // rhs *= weight / history_size
+    if (is_u_kind(kind)) b *= us;  // rhs *= weight / history_size
     bvec[tid] = b;
   }
   __syncthreads();
 
-  // ---- CVaR-MF: one gradient step with the full (stale-upper) matrix ----
-  if (is_grad_kind(kind)) {
+  if (grad) {
+    // ---- CVaR-MF: one gradient step with the full (stale-upper) matrix ----
     if (tid < Dp) {
       const int i = tid, I = i >> 5, ri = i & 31;
       float y = 0.0f;
@@ -307,7 +337,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
         if (j <= i)
           aij = tiles[tidx(I, j >> 5) * 1024 + sw(ri, j & 31)];
         else
-          aij = cvar_upper(kind, a.G[(int64_t)i * Dp + j], a.w, omega);
+          aij = cvar_upper(kind, a.G[i * Dp + j], a.w, omega);
         y += aij * xvec[j];
       }
       a.out[e * Dp + i] = xvec[i] - a.eta * (y - bvec[i]);
@@ -315,82 +345,99 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     return;
   }
 
-  // ---- blocked right-looking Cholesky, rhs as an extra panel row ----
+  // ---- blocked right-looking Cholesky with lookahead ----
+  // Diagonal tiles become L_pp^-1.  Wave 0 updates tile (p+1, p+1) first
+  // and factors it while the other waves finish panel p's trailing update.
+  if (wave == 0 && !(a.debug_skip & 2)) {
+    if (!diag_factor_inv(tiles, lane) && lane == 0) flag[0] = 1;
+  }
+  __syncthreads();
   for (int p = 0; p < T; ++p) {
-    float* Tpp = tiles + tidx(p, p) * 1024;
-    if (wave == 0) {
-      const bool ok = diag_factor(Tpp, ldc, lane);
-      if (!ok && lane == 0) flag[0] = 1;
-    }
-    __syncthreads();
-    const int nrow = 32 * (T - 1 - p) + 1;
-    if (tid < nrow) {
-      float x[32];
-      const bool isb = (tid == nrow - 1);
-      const int I = p + 1 + (tid >> 5), r = tid & 31;
-      float* tl = tiles + tidx(isb ? p : I, p) * 1024;
+    const float* Tpp = tiles + tidx(p, p) * 1024;
+    const int npan = T - 1 - p;
+    // TRSM by MFMA: L_Ip = A_Ip (L_pp^-1)^T ; y_p = L_pp^-1 b_p
+    if (!(a.debug_skip & 4)) {
+      for (int t = wave; t < npan; t += NW) {
+        float* Aip = tiles + tidx(p + 1 + t, p) * 1024;
+        const f32x16 u = tile_pqT(Aip, Tpp, lo, hi);
 #pragma unroll
-      for (int c = 0; c < 32; ++c) x[c] = isb ? bvec[32 * p + c] : tl[sw(r, c)];
-      trsm_row(x, ldc);
-#pragma unroll
-      for (int c = 0; c < 32; ++c) {
-        if (isb) bvec[32 * p + c] = x[c];
-        else tl[sw(r, c)] = x[c];
+        for (int q = 0; q < 16; ++q) Aip[sw(acc_row(q, hi), lo)] = u[q];
+      }
+      if (wave == (npan % NW) && hi == 0) {
+        float y = 0.0f;
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) y += Tpp[sw(lo, k)] * bvec[32 * p + k];
+        xvec[lo] = y;  // staged; copied into bvec after the barrier
       }
     }
     __syncthreads();
+    if (tid < 32) bvec[32 * p + tid] = xvec[tid];
     if (p < T - 1) {
-      const int nb = 32 * (T - 1 - p);
-      if (tid < nb) {  // b_J -= L_Jp y_p
-        const int J = p + 1 + (tid >> 5), r = tid & 31;
+      const int nb = 32 * npan;
+      if (tid >= 64 && tid < 64 + nb) {  // b_J -= L_Jp y_p (y_p still in xvec)
+        const int t2 = tid - 64;
+        const int J = p + 1 + (t2 >> 5), r = t2 & 31;
         const float* L = tiles + tidx(J, p) * 1024;
         float t = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 32; ++k) t += L[sw(r, k)] * bvec[32 * p + k];
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) t += L[sw(r, k)] * xvec[k];
         bvec[32 * J + r] -= t;
       }
-      const int ntr = (T - 1 - p) * (T - p) / 2;
-      for (int tt = wave; tt < ntr; tt += NW) {  // A_IJ -= L_Ip L_Jp^T
-        int Ir = 0;
-        while ((Ir + 1) * (Ir + 2) / 2 <= tt) ++Ir;
-        const int Jr = tt - Ir * (Ir + 1) / 2;
-        const int I = p + 1 + Ir, J = p + 1 + Jr;
-        const float* Lip = tiles + tidx(I, p) * 1024;
-        const float* Ljp = tiles + tidx(J, p) * 1024;
-        f32x16 u = f32x16{0.f};
+      // trailing update A_IJ -= L_Ip L_Jp^T; tile (p+1, p+1) is index 0
+      const int ntr = npan * (npan + 1) / 2;
+      if (wave == 0) {
+        float* A11 = tiles + tidx(p + 1, p + 1) * 1024;
+        const float* L1 = tiles + tidx(p + 1, p) * 1024;
+        if (!(a.debug_skip & 8)) {
+          const f32x16 u = tile_pqT(L1, L1, lo, hi);
 #pragma unroll
-        for (int s = 0; s < 16; ++s)
-          u = mfma32(Lip[sw(lo, 2 * s + hi)], Ljp[sw(lo, 2 * s + hi)], u);
-        float* Aij = tiles + tidx(I, J) * 1024;
+          for (int q = 0; q < 16; ++q) A11[sw(acc_row(q, hi), lo)] -= u[q];
+        }
+        if (!(a.debug_skip & 2)) {
+          if (!diag_factor_inv(A11, lane) && lane == 0) flag[0] = 1;
+        }
+      } else {
+        for (int tt = wave; tt < ntr && !(a.debug_skip & 8); tt += NW - 1) {
+          int Ir = 0;
+          while ((Ir + 1) * (Ir + 2) / 2 <= tt) ++Ir;
+          const int Jr = tt - Ir * (Ir + 1) / 2;
+          const int I = p + 1 + Ir, J = p + 1 + Jr;
+          const f32x16 u = tile_pqT(tiles + tidx(I, p) * 1024, tiles + tidx(J, p) * 1024, lo, hi);
+          float* Aij = tiles + tidx(I, J) * 1024;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) Aij[sw(acc_row(q, hi), lo)] -= u[q];
+          for (int q = 0; q < 16; ++q) Aij[sw(acc_row(q, hi), lo)] -= u[q];
+        }
       }
     }
     __syncthreads();
   }
 
-  // ---- back substitution L^T x = y (wave 0, lane k owns x_k) ----
-  if (wave == 0) {
-    const int k = lo;
-    for (int p = T - 1; p >= 0; --p) {
-      float r = bvec[32 * p + k];
-      for (int q = p + 1; q < T; ++q) {
-        const float* L = tiles + tidx(q, p) * 1024;
-#pragma unroll 8
-        for (int m = 0; m < 32; ++m) r -= L[sw(m, k)] * xvec[32 * q + m];
-      }
-      const float* Lpp = tiles + tidx(p, p) * 1024;
-      float* xp = xvec + 32 * p;
+  // ---- back substitution x = L^-T y with the stored L_pp^-1 ----
+  // r_p = y_p - sum_{q>p} L_qp^T x_q   (one wave per q, partials in LDS)
+  // x_p = (L_pp^-1)^T r_p
+  for (int p = T - 1; p >= 0 && !(a.debug_skip & 16); --p) {
+    const int nq = T - 1 - p;  // < NW: one q per wave
+    if (wave < nq) {
+      const int q = p + 1 + wave;
+      const float* L = tiles + tidx(q, p) * 1024;
+      float pr = 0.0f;
 #pragma unroll 4
-      for (int kk = 31; kk >= 0; --kk) {
-        if (k == kk && hi == 0) xp[kk] = r / Lpp[sw(kk, kk)];
-        __builtin_amdgcn_wave_barrier();
-        const float xk = xp[kk];
-        if (k < kk) r -= Lpp[sw(kk, k)] * xk;
-      }
+      for (int m = 16 * hi; m < 16 * hi + 16; ++m) pr += L[sw(m, lo)] * xvec[32 * q + m];
+      pr += __shfl_xor(pr, 32);
+      if (hi == 0) part[wave * 32 + lo] = pr;
     }
+    __syncthreads();
+    if (wave == 0) {
+      float r = bvec[32 * p + lo];
+      for (int w = 0; w < nq; ++w) r -= part[w * 32 + lo];
+      const float* Tpp = tiles + tidx(p, p) * 1024;
+      float x = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) x += Tpp[sw(i, lo)] * rdlane(r, i);
+      if (hi == 0) xvec[32 * p + lo] = x;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (tid < Dp) a.out[e * Dp + tid] = xvec[tid];
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
@@ -529,13 +576,13 @@ __global__ void __launch_bounds__(256) solve_small_kernel(SolveArgs a) {
 template <int T>
 hipError_t launch_tiled(const SolveArgs& a, hipStream_t s) {
   using C = TiledCfg<T>;
-  static bool attr_set = false;
-  if (!attr_set) {
+  static bool attr = false;
+  if (!attr) {
     hipError_t err = hipFuncSetAttribute((const void*)solve_tiled_kernel<T>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)C::BYTES);
     if (err != hipSuccess) return err;
-    attr_set = true;
+    attr = true;
   }
   hipLaunchKernelGGL(solve_tiled_kernel<T>, dim3((unsigned)a.n_rows), dim3(C::NTHR), C::BYTES, s,
                      a);
