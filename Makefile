@@ -9,6 +9,7 @@ OBJ      := $(PKG)/build
 LIB      := $(PKG)/frecsys_hip/libfrecsys_hip.so
 ORACLE   := oracle/liboracle.so
 RUNMODEL := $(PKG)/bin/run_model
+MODELDUMP := $(PKG)/bin/model_dump
 ARCH     ?= gfx950
 HIPCC    ?= /opt/rocm/bin/hipcc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
@@ -18,11 +19,12 @@ HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/gramian.hip $(CSRC)/loss.hip $(CSRC)/capi.
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h include/frecsys_hip.h
 
-.PHONY: all lib oracle run_model clean
-all: lib oracle
+.PHONY: all lib oracle run_model model_dump clean
+all: lib oracle run_model model_dump
 lib: $(LIB)
 oracle: $(ORACLE)
 run_model: $(RUNMODEL)
+model_dump: $(MODELDUMP)
 
 $(OBJ)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
@@ -42,3 +44,8 @@ $(RUNMODEL): $(PKG)/tools/run_model.cc $(FRECSYS_HDRS) include/frecsys_hip.h $(L
 
 clean:
 	rm -rf $(OBJ) $(LIB) $(ORACLE) $(PKG)/bin
+
+$(MODELDUMP): tests/cpp/model_dump.cc $(FRECSYS_HDRS) include/frecsys_hip.h $(LIB)
+	@mkdir -p $(PKG)/bin
+	g++ $(CXXFLAGS) -o $@ tests/cpp/model_dump.cc -L$(PKG)/frecsys_hip -lfrecsys_hip \
+	    -Wl,-rpath,'$$ORIGIN/../frecsys_hip'

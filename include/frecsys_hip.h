@@ -90,7 +90,9 @@ typedef struct {
   float stepsize;          /* CVaR-MF eta (cvar_mf.h:133) */
   int32_t from_snapshot;   /* 1: X = snapshot of the other side (CVaR StepV
                               uses the pre-step U, cvar_mf.h:282,294) */
-  int32_t reserved;
+  int32_t lambda_is_reg;   /* 1: use `reg` itself as every entity's lambda
+                              (the static Project* API receives the final
+                              lambda, ials.h:88-90) */
   const float* entity_weight; /* host [rows of side]: omega_u (WEIGHTED_U,
                                  CVAR_GRAD_U); NULL -> 1 */
   const float* entity_reg;    /* host [rows of side]: item_reg_[v]
@@ -142,6 +144,10 @@ int frecsys_snapshot(frecsys_ctx* ctx, int32_t side);
  * [rows of side] or NULL.  host_out (dim x dim, row-major) may be NULL. */
 int frecsys_gramian(frecsys_ctx* ctx, int32_t side, const float* weights,
                     int32_t from_snapshot, float* host_out);
+/* Overwrite G[side] with a host dim x dim matrix (row-major, leading dim
+ * ld) -- the static Project* entry points take an arbitrary Gramian. */
+int frecsys_set_gramian(frecsys_ctx* ctx, int32_t side, const float* host,
+                        int64_t ld);
 /* Solve every row of `side` owned by this rank against the other side's
  * embeddings and G[other side]; rows with an empty history are left
  * untouched.  USER/ITEM results are then all-gathered across ranks.  EVAL

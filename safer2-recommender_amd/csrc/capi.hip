@@ -565,6 +565,17 @@ int frecsys_gramian(frecsys_ctx* c, int32_t side, const float* weights, int32_t 
   return FRECSYS_OK;
 }
 
+int frecsys_set_gramian(frecsys_ctx* c, int32_t side, const float* host, int64_t ld) {
+  if (!c || side < 0 || side > 1 || !host || ld < c->dim)
+    return fail(c, FRECSYS_ERR_INVALID, "set_gramian: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipMemsetAsync(c->gram[side], 0, sizeof(float) * c->Dp * c->Dp, c->stream));
+  HIP_TRY(c, hipMemcpy2DAsync(c->gram[side], sizeof(float) * c->Dp, host, sizeof(float) * ld,
+                              sizeof(float) * c->dim, c->dim, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
 int frecsys_solve_side(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p) {
   if (!c || !valid_side(side) || !p) return fail(c, FRECSYS_ERR_INVALID, "solve: bad arguments");
   if (!c->rp[side]) return fail(c, FRECSYS_ERR_INVALID, "solve: no CSR loaded for side");
@@ -617,6 +628,7 @@ int frecsys_solve_side(frecsys_ctx* c, int32_t side, const frecsys_solve_params*
   a.w = p->unobserved_weight;
   a.alpha = p->alpha;
   a.eta = p->stepsize;
+  a.lambda_is_reg = p->lambda_is_reg;
   a.entity_weight = (ukind && p->entity_weight) ? c->d_entity_weight : nullptr;
   a.entity_reg = vkind ? c->d_entity_reg : nullptr;
   a.other_weight = vkind ? c->d_other_weight : nullptr;

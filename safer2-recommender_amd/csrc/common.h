@@ -50,7 +50,9 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 //  V kinds: ItemRegularizationValue, safer2.h:426-432
 __device__ __forceinline__ float entity_lambda(int kind, float reg, float reg_exp, float w,
                                                float alpha, int64_t h, int64_t n_other,
-                                               const float* entity_reg, int64_t e) {
+                                               const float* entity_reg, int64_t e,
+                                               int lambda_is_reg = 0) {
+  if (lambda_is_reg) return reg;
   if (kind == KIND_IALS) return reg * powf((float)h + w * (float)n_other, reg_exp);
   if (is_u_kind(kind)) return reg * (1.0f + w * (float)n_other);
   return reg * (entity_reg[e] + alpha * w * (float)n_other);

@@ -31,6 +31,7 @@ struct SolveArgs {
   const float* E;           // current embeddings of the solved side (CVaR)
   float* out;               // solved side's embeddings, ld = Dp
   float reg, reg_exp, w, alpha, eta;
+  int lambda_is_reg;           // lambda = reg for every entity
   const float* entity_weight;  // [rows of side] omega, or nullptr (-> 1)
   const float* entity_reg;     // [rows of side] item_reg_
   const float* other_weight;   // [rows of other side] nu

@@ -232,7 +232,8 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
   const float hf = (float)h;
   const float omega = (is_u_kind(kind) && a.entity_weight) ? a.entity_weight[e] : 1.0f;
   const float lam =
-      entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other, a.entity_reg, e);
+      entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other, a.entity_reg, e,
+                    a.lambda_is_reg);
   const bool grad = is_grad_kind(kind);
   const float gscale = kind == KIND_IALS ? a.w : (is_u_kind(kind) ? hf * a.w : a.w);
   f32x16 acc[MT];
@@ -517,7 +518,7 @@ __global__ void __launch_bounds__(256) solve_small_kernel(SolveArgs a) {
   const float hf = (float)h;
   const float omega = (is_u_kind(kind) && a.entity_weight) ? a.entity_weight[e] : 1.0f;
   const float lam = entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other,
-                                  a.entity_reg, e);
+                                  a.entity_reg, e, a.lambda_is_reg);
 #pragma unroll
   for (int t = 0; t < PER; ++t) {
     const int el = lane * PER + t, i = el / Dp, j = el % Dp;

@@ -32,7 +32,7 @@ EXPORTS = (
     "frecsys_partition", "frecsys_comm_unique_id", "frecsys_comm_init",
     "frecsys_shard_range", "frecsys_load_csr", "frecsys_set_embeddings",
     "frecsys_get_embeddings", "frecsys_init_embeddings", "frecsys_snapshot",
-    "frecsys_gramian", "frecsys_solve_side", "frecsys_user_loss",
+    "frecsys_gramian", "frecsys_set_gramian", "frecsys_solve_side", "frecsys_user_loss",
     "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset",
 )
 
@@ -54,7 +54,7 @@ class _SolveParams(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("reg", ctypes.c_float),
                 ("reg_exp", ctypes.c_float), ("unobserved_weight", ctypes.c_float),
                 ("alpha", ctypes.c_float), ("stepsize", ctypes.c_float),
-                ("from_snapshot", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("from_snapshot", ctypes.c_int32), ("lambda_is_reg", ctypes.c_int32),
                 ("entity_weight", ctypes.c_void_p), ("entity_reg", ctypes.c_void_p),
                 ("other_weight", ctypes.c_void_p)]
 
@@ -88,6 +88,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_init_embeddings": (ctypes.c_int, [P, ctypes.c_uint32, F]),
         "frecsys_snapshot": (ctypes.c_int, [P, I32]),
         "frecsys_gramian": (ctypes.c_int, [P, I32, P, I32, P]),
+        "frecsys_set_gramian": (ctypes.c_int, [P, I32, P, I64]),
         "frecsys_solve_side": (ctypes.c_int, [P, I32, P]),
         "frecsys_user_loss": (ctypes.c_int, [P, I32, F, I32, P]),
         "frecsys_synchronize": (ctypes.c_int, [P]),

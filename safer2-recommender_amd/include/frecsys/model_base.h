@@ -1,0 +1,213 @@
+// model_base.h -- state and helpers shared by the four GPU model classes.
+//
+// Host-resident: the small per-user vectors of the reference models
+// (user_loss_, dual_weight_, user_history_size_, item_reg_; safer2.h:841-847)
+// and the print flags.  Device-resident (DeviceContext): U, V, Gramians,
+// the CSR of the training set.  The static per-entity entry points
+// (Project / ProjectU / ProjectV of the reference) run on the GPU through a
+// one-row context (ProjectOnDevice).
+#pragma once
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "frecsys/dataset.h"
+#include "frecsys/device.h"
+#include "frecsys/evaluation.h"
+#include "frecsys/logging.h"
+#include "frecsys/recommender.h"
+#include "frecsys/types.h"
+
+namespace frecsys {
+namespace detail {
+
+class DeviceModel : public Recommender {
+ public:
+  DeviceModel(int dim, int num_users, int num_items, float stdev, const DeviceOptions& opts)
+      : dim_(dim), num_users_(num_users), num_items_(num_items), opts_(opts) {
+    dev_ = std::make_unique<DeviceContext>(dim, num_users, num_items, opts);
+    // adjusted_stdev = stdev / sqrt(dim); U then V from one mt19937
+    // (ials.h:47-51 / recommender.h:61-67)
+    dev_->InitEmbeddings(opts.seed, stdev);
+  }
+
+  void SetPrintTrainStats(const bool v) override { print_trainstats_ = v; }
+  void SetPrintResidualStats(const bool v) override { print_residualstats_ = v; }
+  void SetPrintVarStats(const bool v) override { print_varstats_ = v; }
+
+  // Host copies of the device embeddings (item_embedding(), ials.h:410).
+  MatrixXf item_embedding() const { return dev_->Get(DeviceContext::ITEM); }
+  MatrixXf user_embedding() const { return dev_->Get(DeviceContext::USER); }
+  void set_embeddings(const MatrixXf& U, const MatrixXf& V) {
+    dev_->Set(DeviceContext::USER, U);
+    dev_->Set(DeviceContext::ITEM, V);
+    OnEmbeddingsSet();
+  }
+  const VectorXf& user_loss() const { return user_loss_; }
+  DeviceContext& device() { return *dev_; }
+
+ protected:
+  virtual void OnEmbeddingsSet() {}
+
+  // Fold-in + scoring (ials.h:148-185 and its model variants): project the
+  // users of `data` with `params` on the GPU, then rank on host.
+  EvaluationResult FoldInEvaluate(const VectorXi& k_list, const VectorXf& alpha_list,
+                                  const Dataset& data, const SpMatrix& eval_by_user,
+                                  const frecsys_solve_params& params) {
+    std::vector<int32_t> ids;
+    Csr csr;
+    data.compact_users(&ids, &csr);
+    dev_->LoadEval(csr);
+    dev_->Solve(DeviceContext::EVAL, params);
+    const MatrixXf Ue = dev_->Get(DeviceContext::EVAL);
+    const MatrixXf V = dev_->Get(DeviceContext::ITEM);
+    std::unordered_map<int, int> user_to_ind;
+    for (size_t i = 0; i < ids.size(); ++i) user_to_ind[ids[i]] = (int)i;
+    std::unordered_map<int, int> row_of;
+    int n = 0;
+    for (const auto& kv : eval_by_user) row_of[kv.first] = n++;
+    const int64_t d = dim_;
+    return EvaluateDatasetInternal(
+        (int)num_items_, k_list, alpha_list, row_of, data, eval_by_user,
+        [&](const int user_id, const SpVector&) {
+          VectorXf s(V.rows());
+          const float* u = Ue.row(user_to_ind.at(user_id));
+          for (int64_t i = 0; i < V.rows(); ++i) {
+            const float* v = V.row(i);
+            float t = 0.f;
+            for (int64_t k = 0; k < d; ++k) t += v[k] * u[k];
+            s[i] = t;
+          }
+          return s;
+        });
+  }
+
+  // Initialize() bookkeeping of ERM-MF / CVaR-MF / SAFER2
+  // (safer2.h:827-837): |H_u| and item_reg_[v] = sum_{u in H_v} 1/|H_u|
+  // accumulated in by_item (file) order.
+  void ComputeHistoryStats(const Dataset& data) {
+    user_history_size_ = VectorXf::Zero(num_users_);
+    item_reg_ = VectorXf::Zero(num_items_);
+    const Csr& u = data.user_csr();
+    const Csr& it = data.item_csr();
+    for (int64_t r = 0; r < u.rows() && r < num_users_; ++r) user_history_size_[r] = (float)u.len(r);
+    for (int64_t v = 0; v < it.rows() && v < num_items_; ++v)
+      for (int64_t k = it.ptr[v]; k < it.ptr[v + 1]; ++k)
+        item_reg_[v] = (float)((double)item_reg_[v] + 1.0 / (double)user_history_size_[it.col[k]]);
+  }
+
+  // VaR / CVaR of the user losses (safer2.h:304-316).
+  void PrintVarStats(float alpha) const {
+    std::vector<float> vals((size_t)user_loss_.size());
+    for (int64_t i = 0; i < user_loss_.size(); ++i) vals[i] = -user_loss_[i];
+    const size_t Q = (size_t)((float)vals.size() * alpha);
+    std::nth_element(vals.begin(), vals.begin() + Q, vals.end());
+    float loss = 0;
+    for (size_t i = 0; i <= Q; i++) loss += -vals[i];
+    LOG(INFO) << "VaR: " << -vals[Q] << " CVaR: " << loss / (float)Q;
+  }
+
+  // Train-loss diagnostics (ials.h:226-305, safer2.h:337-413).  Host-side
+  // diagnostics over downloaded embeddings; counted in Train() time like
+  // the reference's (run_model flag --print_train_stats).
+  struct LossParts {
+    double observed = 0, reg_user_now = 0, reg_item_now = 0, unobserved = 0;
+  };
+  LossParts ComputeLossParts(const Dataset& data) {
+    LossParts lp;
+    const MatrixXf U = dev_->Get(DeviceContext::USER), V = dev_->Get(DeviceContext::ITEM);
+    const Csr& u = data.user_csr();
+    float obs = 0.f;
+    for (int64_t r = 0; r < u.rows(); ++r)
+      for (int64_t k = u.ptr[r]; k < u.ptr[r + 1]; ++k) {
+        float p = 0.f;
+        for (int j = 0; j < dim_; ++j) p += V(u.col[k], j) * U(r, j);
+        obs += (p - 1.0f) * (p - 1.0f);
+      }
+    lp.observed = obs;
+    std::vector<double> gu((size_t)dim_ * dim_, 0.0), gv((size_t)dim_ * dim_, 0.0);
+    for (int64_t r = 0; r < U.rows(); ++r)
+      for (int i = 0; i < dim_; ++i)
+        for (int j = 0; j < dim_; ++j) gu[(size_t)i * dim_ + j] += (double)U(r, i) * U(r, j);
+    for (int64_t r = 0; r < V.rows(); ++r)
+      for (int i = 0; i < dim_; ++i)
+        for (int j = 0; j < dim_; ++j) gv[(size_t)i * dim_ + j] += (double)V(r, i) * V(r, j);
+    for (size_t i = 0; i < gu.size(); ++i) lp.unobserved += gu[i] * gv[i];
+    return lp;
+  }
+
+  static double RowSqNorm(const MatrixXf& M, int64_t r) {
+    double s = 0;
+    for (int64_t j = 0; j < M.cols(); ++j) s += (double)M(r, j) * M(r, j);
+    return s;
+  }
+
+  void CheckNaN(float loss) const {
+    if (std::isnan(loss)) {  // ials.h:291-296: logged, then exit(0)
+      LOG(ERROR) << "!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!";
+      LOG(ERROR) << "NaN is detected!!";
+      LOG(ERROR) << "!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!!";
+      std::exit(0);
+    }
+  }
+
+  int dim_;
+  int64_t num_users_, num_items_;
+  DeviceOptions opts_;
+  std::unique_ptr<DeviceContext> dev_;
+  VectorXf user_loss_;
+  VectorXf dual_weight_;
+  VectorXf user_history_size_;
+  VectorXf item_reg_;
+  bool print_trainstats_ = false;
+  bool print_residualstats_ = false;  // uninitialised in the reference
+  bool print_varstats_ = false;
+};
+
+inline void check_ok(int rc) {
+  if (rc != FRECSYS_OK) LOG(FATAL) << "frecsys call failed (" << rc << "): " << frecsys_last_error(nullptr);
+}
+
+// One-entity projection through a temporary device context: the reference's
+// static Project / ProjectU / ProjectV (ials.h:88, safer2.h:104, 166) with
+// `reg` used as the final lambda.
+inline VectorXf ProjectOnDevice(int kind, const SpVector& history, const MatrixXf& X,
+                                const MatrixXf& G, float reg, float w, float weight,
+                                const VectorXf* nu) {
+  const int d = (int)X.cols();
+  DeviceOptions o;
+  o.world = 1;
+  o.rank = 0;
+  DeviceContext ctx(d, 1, X.rows(), o);
+  Csr c;
+  c.ptr = {0, (int64_t)history.size()};
+  for (const auto& p : history) c.col.push_back(p.first);
+  // side USER (1 row) against ITEM = X
+  check_ok(frecsys_load_csr(ctx.raw(), FRECSYS_SIDE_USER, 1, c.ptr.data(), c.col.data()));
+  ctx.Set(DeviceContext::ITEM, X);
+  check_ok(frecsys_set_gramian(ctx.raw(), FRECSYS_SIDE_ITEM, G.data(), d));
+  frecsys_solve_params p = solve_params(kind, reg, w);
+  p.lambda_is_reg = 1;
+  float om = weight;
+  std::vector<float> er(1, 0.0f);
+  std::vector<float> nuv;
+  if (kind == FRECSYS_KIND_WEIGHTED_U) p.entity_weight = &om;
+  if (kind == FRECSYS_KIND_WEIGHTED_V) {
+    nuv.assign(nu->data(), nu->data() + nu->size());
+    p.entity_reg = er.data();
+    p.other_weight = nuv.data();
+  }
+  ctx.Solve(DeviceContext::USER, p);
+  MatrixXf out = ctx.Get(DeviceContext::USER);
+  VectorXf x(d);
+  for (int j = 0; j < d; ++j) x[j] = out(0, j);
+  return x;
+}
+
+}  // namespace detail
+}  // namespace frecsys

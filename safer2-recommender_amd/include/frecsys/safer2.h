@@ -1,0 +1,312 @@
+// safer2.h -- SAFER2 on MI355X (reference safer2.h:35-871, same surface).
+//
+// Train() (safer2.h:266-334): for each primal-dual iteration the dual
+// weights omega from the cached losses and xi (host, double math as the
+// reference's erfc/exp), StepU (FRECSYS_KIND_WEIGHTED_U against the cached
+// item Gramian), StepV (Gramian U^T diag(omega) U, nu = omega/|H_u|,
+// FRECSYS_KIND_WEIGHTED_V with the tail quirk), item_gramian_ = V^T V,
+// ComputeUserLoss; then xi by smoothed-quantile Newton with Armijo.
+#pragma once
+
+#include <cmath>
+#include <random>
+#include <tuple>
+#include <vector>
+
+#include "frecsys/model_base.h"
+
+namespace frecsys {
+namespace quantile {
+
+// Kernel helpers, safer2.h:598-647.  Float arguments, double intermediates,
+// float results -- the promotions of the source expressions.
+inline float gaussian_kernel(const float u, const float h) {
+  return (float)(std::pow(2 * M_PI, -0.5) * std::exp(-std::pow((double)(u / h) * M_SQRT1_2, 2)) /
+                 h);
+}
+inline float gaussian_kernel_cdf(const float u, const float h) {
+  return (float)(0.5 * std::erfc(-(double)(u / h) * M_SQRT1_2));
+}
+inline float gaussian_loss(const float u, const float h, const float alpha) {
+  const float ell = h * gaussian_kernel(u, h) + (u / h) * (1 - 2 * gaussian_kernel_cdf(-u, h));
+  return (float)((double)((h / 2) * ell) + ((double)(1 - alpha) - 0.5) * (double)u);
+}
+inline float epanechnikov_kernel(const float u, const float h) {
+  const float uh = u / h;
+  return (float)((3.0 / 4.0) * (1 - std::pow((double)uh, 2)) * (int)(std::fabs(uh) < 1) / h);
+}
+inline float epanechnikov_kernel_cdf(const float u, const float h) {
+  const float uh = u / h;
+  const int in_supp = (int)(std::fabs(uh) <= 1);
+  const int pos = (int)(uh > 1);
+  return (float)(((std::pow((double)h, -3) / 4.0) *
+                  ((3 * (double)u * std::pow((double)h, 2) - std::pow((double)u, 3)) +
+                   2 * std::pow((double)h, 3)) *
+                  in_supp) +
+                 (double)((1 - in_supp) * pos));
+}
+inline float epanechnikov_loss(const float u, const float h, const float alpha) {
+  const float uh = u / h;
+  const int in_supp = (int)(std::fabs(uh) <= 1);
+  const int pos = (int)(uh > 1);
+  const float ell = (float)(((3.0 / 4.0) * std::pow((double)uh, 2) -
+                             (1.0 / 8.0) * std::pow((double)uh, 4) + (3.0 / 8.0)) *
+                                in_supp +
+                            (double)(std::fabs(uh) * pos));
+  return (float)((1.0 / 2.0) * h * ell + ((double)(1 - alpha) - 0.5) * (double)u);
+}
+
+struct Smoother {
+  float alpha, bandwidth;
+  bool epan;
+  // EvaluateQuantile (safer2.h:652-689): value, gradient, Hessian of the
+  // smoothed quantile objective at xi; means accumulated in double.
+  std::tuple<float, float, float> Evaluate(float xi, const float* loss, int64_t n) const {
+    double sc = 0, sk = 0, sl = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      const float u = loss[i] - xi;
+      if (epan) {
+        sc += epanechnikov_kernel_cdf(-u, bandwidth);
+        sk += epanechnikov_kernel(-u, bandwidth);
+        sl += epanechnikov_loss(u, bandwidth, alpha);
+      } else {
+        sc += gaussian_kernel_cdf(-u, bandwidth);
+        sk += gaussian_kernel(-u, bandwidth);
+        sl += gaussian_loss(u, bandwidth, alpha);
+      }
+    }
+    const float grad = (-(1 - alpha) + (float)(sc / (double)n)) / alpha;
+    const float H = (float)(sk / (double)n) / alpha;
+    const float value = (float)(sl / (double)n) / alpha;
+    return {value, grad, H};
+  }
+  // ComputeXiDirection (safer2.h:692-712): Newton step with Armijo
+  // backtracking (c = 1e-4, <= 32 halvings, gradient at the trial point).
+  float Direction(float xi, const float* loss, int64_t n) const {
+    auto [f0, g0, H] = Evaluate(xi, loss, n);
+    const float d = g0 / H;
+    const float c = 1e-4f;
+    float gamma = 1.0f;
+    float x = xi + gamma * (-d);
+    for (int k = 0; k < 32; k++) {
+      auto [fx, gx, Hx] = Evaluate(x, loss, n);
+      (void)Hx;
+      if (fx > f0 + c * gamma * gx * (-d)) {
+        gamma *= 0.5f;
+        x = xi + gamma * (-d);
+      } else {
+        break;
+      }
+    }
+    return -gamma * d;
+  }
+  float Weight(float loss, float xi) const {  // safer2.h:770-776
+    const float r = loss - xi;
+    return epan ? 1 - epanechnikov_kernel_cdf(-r, bandwidth) : 1 - gaussian_kernel_cdf(-r, bandwidth);
+  }
+};
+
+}  // namespace quantile
+
+class SAFER2Recommender : public detail::DeviceModel {
+ public:
+  SAFER2Recommender(int embedding_dim, int num_users, int num_items, float reg,
+                    float unobserved_weight, float bandwidth, float alpha, float stdev,
+                    int xi_iterations, int pd_iterations, bool use_epanechnikov, bool use_snr,
+                    float sampling_ratio, bool use_cg, float cg_error_tolerance,
+                    int cg_max_iterations, const DeviceOptions& opts = DeviceOptions::FromEnv())
+      : DeviceModel(embedding_dim, num_users, num_items, stdev, opts),
+        smoother_{alpha, bandwidth, use_epanechnikov} {
+    if (use_cg) LOG(FATAL) << "use_cg is not supported by the MI355X solve loop (LLT path only)";
+    (void)cg_error_tolerance;
+    (void)cg_max_iterations;
+    regularization_ = reg;
+    unobserved_weight_ = unobserved_weight;
+    bandwidth_ = bandwidth;
+    alpha_ = alpha;
+    use_epanechnikov_ = use_epanechnikov;
+    prev_xi_ = 0.0f;
+    xi_iterations_ = xi_iterations;
+    use_snr_ = use_snr;
+    sampling_ratio_ = sampling_ratio;
+    pd_iterations_ = pd_iterations;
+    snr_rng_.seed(opts.seed >= 0 ? (uint32_t)(opts.seed + 7919) : std::random_device{}());
+    dual_weight_ = VectorXf::Constant(num_users, alpha);  // safer2.h:56
+    user_loss_ = VectorXf::Zero(num_users);
+    user_history_size_ = VectorXf::Zero(num_users);
+    item_reg_ = VectorXf::Zero(num_items);
+    dev_->Gramian(DeviceContext::ITEM);  // item_gramian_ = V^T V, safer2.h:55
+  }
+
+  VectorXf Score(const int, const SpVector&) override {
+    throw("Function 'Score' is not implemented");  // safer2.h:79-82
+  }
+
+  static const VectorXf ProjectU(const SpVector& user_history, const MatrixXf& item_embeddings,
+                                 const MatrixXf& gramian, const float reg,
+                                 const float unobserved_weight, const float weight, bool use_cg,
+                                 const float = 1e-10, const int = 100) {
+    if (use_cg) LOG(FATAL) << "use_cg is not supported";
+    return detail::ProjectOnDevice(FRECSYS_KIND_WEIGHTED_U, user_history, item_embeddings,
+                                   gramian, reg, unobserved_weight, weight, nullptr);
+  }
+  static const VectorXf ProjectV(const SpVector& item_history, const MatrixXf& user_embeddings,
+                                 const MatrixXf& gramian, const float reg,
+                                 const float unobserved_weight, const VectorXf& dual_weight,
+                                 bool use_cg, const float = 1e-10, const int = 100) {
+    if (use_cg) LOG(FATAL) << "use_cg is not supported";
+    return detail::ProjectOnDevice(FRECSYS_KIND_WEIGHTED_V, item_history, user_embeddings,
+                                   gramian, reg, unobserved_weight, 1.0f, &dual_weight);
+  }
+
+  EvaluationResult EvaluateDataset(const VectorXi& k_list, const VectorXf& alpha_list,
+                                   const Dataset& data, const SpMatrix& eval_by_user) override {
+    // StepU with omega = 1 and the cached item gramian (safer2.h:246-252)
+    return FoldInEvaluate(k_list, alpha_list, data, eval_by_user, u_params(false));
+  }
+
+  void Train(const Dataset& data) override {
+    dev_->LoadTraining(data);
+    PrintLosses(data);
+    for (int t = 0; t < pd_iterations_; ++t) {
+      ComputeUserWeights(data);                                   // safer2.h:272-273
+      frecsys_solve_params pu = u_params(true);
+      dev_->Solve(DeviceContext::USER, pu);                       // safer2.h:277-285
+      StepV(data);                                                // safer2.h:288-290
+      dev_->Gramian(DeviceContext::ITEM);                         // safer2.h:294-295
+      dev_->UserLoss(DeviceContext::USER, unobserved_weight_, true, user_loss_.data());
+      VectorXf wl(num_users_);
+      for (int64_t u = 0; u < num_users_; ++u) wl[u] = dual_weight_[u] * user_loss_[u];
+      LOG(INFO) << "Weighted Loss: " << wl.mean();                // safer2.h:300-301
+      if (print_varstats_) {
+        PrintVarStats(alpha_);
+        LOG(INFO) << format("Min: {0:.3f}, Mean: {1:.3f}, Max: {2:.3f}", dual_weight_.minCoeff(),
+                            dual_weight_.mean(), dual_weight_.maxCoeff());
+      }
+      if (print_residualstats_)
+        LOG(INFO) << format("U residual: {0}, V residual: {1}, z residual: {2}", 0.0f, 0.0f, 0.0f);
+    }
+    const float xi = ComputeXi(user_loss_, prev_xi_, xi_iterations_);  // safer2.h:331-333
+    LOG(INFO) << "Xi:" << xi;
+    prev_xi_ = xi;
+  }
+
+  // Initialize (safer2.h:819-838).
+  void Initialize(const Dataset& data) {
+    dev_->LoadTraining(data);
+    dev_->Gramian(DeviceContext::ITEM);
+    dev_->UserLoss(DeviceContext::USER, unobserved_weight_, true, user_loss_.data());
+    const float prev_xi = user_loss_.mean();
+    const float xi = ComputeXi(user_loss_, prev_xi, xi_iterations_);
+    LOG(INFO) << "Initial Xi:" << xi;
+    prev_xi_ = xi;
+    ComputeHistoryStats(data);
+  }
+
+  // Smoothed-quantile Newton (safer2.h:716-742); use_snr subsamples
+  // N_u * sampling_ratio losses per iteration (seeded when --seed is set).
+  float ComputeXi(const VectorXf& user_loss, const float prev_xi, const int nr_iterations) {
+    float xi = prev_xi;
+    const int64_t n = user_loss.size();
+    for (int t = 0; t < nr_iterations; ++t) {
+      float d;
+      if (!use_snr_) {
+        d = smoother_.Direction(xi, user_loss.data(), n);
+      } else {
+        std::uniform_int_distribution<int> uni(0, (int)n - 1);
+        const int ns = (int)(n * sampling_ratio_);
+        std::vector<float> sample((size_t)ns);
+        for (int j = 0; j < ns; j++) sample[j] = user_loss[uni(snr_rng_)];
+        d = smoother_.Direction(xi, sample.data(), ns);
+      }
+      xi = xi + d;
+    }
+    return xi;
+  }
+
+  float GetMeanWeight() const { return dual_weight_.mean(); }  // safer2.h:815-817
+  float xi() const { return prev_xi_; }
+  const VectorXf& dual_weight() const { return dual_weight_; }
+
+ protected:
+  void OnEmbeddingsSet() override { dev_->Gramian(DeviceContext::ITEM); }
+
+ private:
+  // ComputeUserWeights (safer2.h:745-794): only users with a history.
+  void ComputeUserWeights(const Dataset& data) {
+    const Csr& uc = data.user_csr();
+    for (int64_t u = 0; u < uc.rows() && u < num_users_; ++u)
+      if (uc.len(u)) dual_weight_[u] = smoother_.Weight(user_loss_[u], prev_xi_);
+  }
+
+  // StepV (safer2.h:493-555).
+  void StepV(const Dataset& data) {
+    (void)data;
+    std::vector<float> nu((size_t)num_users_);
+    for (int64_t u = 0; u < num_users_; ++u) nu[u] = dual_weight_[u] / user_history_size_[u];
+    dev_->Gramian(DeviceContext::USER, dual_weight_.data(), ++weight_epoch_);  // :504-509
+    frecsys_solve_params p = solve_params(FRECSYS_KIND_WEIGHTED_V, regularization_,
+                                          unobserved_weight_);
+    p.alpha = alpha_;
+    p.entity_reg = item_reg_.data();
+    p.other_weight = nu.data();
+    dev_->Solve(DeviceContext::ITEM, p);
+  }
+
+  frecsys_solve_params u_params(bool with_weights) const {
+    frecsys_solve_params p = solve_params(FRECSYS_KIND_WEIGHTED_U, regularization_,
+                                          unobserved_weight_);
+    p.entity_weight = with_weights ? dual_weight_.data() : nullptr;
+    return p;
+  }
+
+  // PrintLosses (safer2.h:337-413), diagnostics only.
+  void PrintLosses(const Dataset& data) {
+    if (!print_trainstats_) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    const LossParts lp = ComputeLossParts(data);
+    const MatrixXf U = dev_->Get(DeviceContext::USER), V = dev_->Get(DeviceContext::ITEM);
+    const Csr& uc = data.user_csr();
+    const Csr& ic = data.item_csr();
+    float loss_reg = 0.0f, reg_user_now = 0.0f, reg_item_now = 0.0f;
+    for (int64_t u = 0; u < uc.rows(); ++u) {
+      if (!uc.len(u)) continue;
+      const float n2 = (float)RowSqNorm(U, u);
+      loss_reg += n2 * (regularization_ * (1 + unobserved_weight_ * num_items_));
+      reg_user_now += n2;
+    }
+    for (int64_t i = 0; i < ic.rows(); ++i) {
+      if (!ic.len(i)) continue;
+      const float n2 = (float)RowSqNorm(V, i);
+      loss_reg += n2 * (regularization_ * (item_reg_[i] + alpha_ * unobserved_weight_ * num_users_));
+      reg_item_now += n2;
+    }
+    const float loss = user_loss_.sum();
+    const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                        std::chrono::steady_clock::now() - t0)
+                        .count();
+    CheckNaN(loss);
+    LOG(INFO) << format(
+        "Loss={0:.2f} Loss_observed={1:.2f} Loss_unobserved={2:.2f} Loss_reg={3:.2f} "
+        "Loss_reg (user)={4:.2f} Loss_reg (item)={5:.2f}",
+        loss, lp.observed / data.num_tuples(), lp.unobserved / num_items_ / num_users_, loss_reg,
+        reg_user_now / num_users_, reg_item_now / num_items_);
+    LOG(INFO) << format("Time={0}", (int64_t)ms);
+  }
+
+  quantile::Smoother smoother_;
+  float regularization_;
+  float unobserved_weight_;
+  float bandwidth_;
+  float alpha_;
+  float prev_xi_;
+  bool use_epanechnikov_;
+  int xi_iterations_;
+  bool use_snr_;
+  float sampling_ratio_;
+  int pd_iterations_;
+  uint64_t weight_epoch_ = 0;
+  std::mt19937 snr_rng_;
+};
+
+}  // namespace frecsys

@@ -1,0 +1,153 @@
+"""Whole-model parity and the reference's quality gates, through the
+product's own C++ host layer (include/frecsys/*.h over libfrecsys_hip.so):
+
+* tests/cpp/model_dump runs the C++ model classes with a fixed seed and the
+  reference test hyper-parameters; its embeddings after E Train() epochs are
+  compared with the CPU oracle's Train() trajectory from the same seed;
+* run_model (the CLI) is run on the ML-1M fixture with the reference tests'
+  settings and must pass their gates: NDCG@20 >= 0.2 (ials_test.cc:45,
+  erm_mf_test.cc:45, cvar_mf_test.cc:46, safer2_test.cc:99) and, for
+  SAFER2, mean dual weight within alpha +- 0.02 after every epoch
+  (safer2_test.cc:135, 230).
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import ML1M, PKG, rel_rows
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(PKG, "bin")
+TRAIN = os.path.join(ML1M, "train.csv")
+VTR = os.path.join(ML1M, "validation_tr.csv")
+VTE = os.path.join(ML1M, "validation_te.csv")
+
+
+def _read_dump(path, epochs, with_ndcg):
+    raw = open(path, "rb").read()
+    nu, ni, d = np.frombuffer(raw[:24], np.int64)
+    off = 24
+    f = np.frombuffer(raw[off:], np.float32)
+    U = f[:nu * d].reshape(nu, d)
+    V = f[nu * d:nu * d + ni * d].reshape(ni, d)
+    o = nu * d + ni * d
+    loss = f[o:o + nu]
+    dw = f[o + nu:o + 2 * nu]
+    xi = f[o + 2 * nu]
+    mw = f[o + 2 * nu + 1:o + 2 * nu + 1 + epochs]
+    nd = f[o + 2 * nu + 1 + epochs:] if with_ndcg else None
+    return U, V, loss, dw, float(xi), mw, nd
+
+
+CASES = {
+    # model: (oracle id, reg, w, alpha, bandwidth, stepsize, epan)
+    "ials": (O.MODEL_IALS, 0.003, 0.1, 0.3, 1.0, 0.1, 0),
+    "erm_mf": (O.MODEL_ERM, 0.005, 0.004, 0.3, 1.0, 0.1, 0),
+    "cvar_mf": (O.MODEL_CVAR, 0.002, 0.008, 0.3, 1.0, 0.4, 0),
+    "safer2": (O.MODEL_SAFER2, 0.004, 0.004, 0.3, 0.15, 0.1, 0),
+    "safer2_epan": (O.MODEL_SAFER2, 0.004, 0.004, 0.3, 0.7, 0.1, 1),
+}
+
+
+@pytest.fixture(scope="module")
+def ml1m_csr(ml1m):
+    tr, vt, ve = ml1m
+    up, uc = tr.by_user()
+    ip, ic = tr.by_item()
+    return tr.max_user + 1, tr.max_item + 1, up, uc, ip, ic
+
+
+@pytest.mark.parametrize("case", sorted(CASES))
+@pytest.mark.parametrize("dim", [8, 32])
+def test_train_trajectory_matches_oracle(tmp_path, ml1m_csr, case, dim):
+    model = case.split("_epan")[0]
+    oid, reg, w, alpha, bw, eta, epan = CASES[case]
+    # CVaR-MF's dual weights are a hard threshold (loss - xi >= 0,
+    # cvar_mf.h:623) at the exact quantile of the losses, so from epoch 2 on
+    # users within fp32 summation noise of xi can flip 0 <-> 1 and move whole
+    # item rows.  Its first epoch has xi = 0 (Initialize leaves prev_xi_ at 0,
+    # cvar_mf.h:710-726), so every weight is 1 and the epoch is flip-free;
+    # later epochs are covered by the quality gate below.
+    epochs = 1 if oid == O.MODEL_CVAR else 3
+    out = tmp_path / "dump.bin"
+    subprocess.run([os.path.join(BIN, "model_dump"), model, str(dim), str(epochs), "1", TRAIN,
+                    str(out), str(reg), str(w), str(alpha), str(bw), str(eta), str(epan)],
+                   check=True, capture_output=True, timeout=300)
+    U, V, loss, dw, xi, mw, _ = _read_dump(str(out), epochs, False)
+    nu, ni, up, uc, ip, ic = ml1m_csr
+    m = O.Model(oid, dim, nu, ni, reg=reg, w=w, alpha=alpha, bandwidth=bw, stepsize=eta,
+                epan=bool(epan), seed=1)
+    m.set_data(up, uc, ip, ic)
+    m.initialize()
+    for _ in range(epochs):
+        assert m.train() == 0
+    Uo, Vo = m.embeddings()
+    lo, wo, xo = m.state()
+    # per-row relative error after `epochs` full epochs from the same seed
+    eu, ev = rel_rows(U, Uo), rel_rows(V, Vo)
+    assert np.percentile(ev, 99.9) < 1e-4 and ev.max() < 1e-3, (ev.max(), np.percentile(ev, 99.9))
+    assert np.percentile(eu, 99.9) < 1e-4 and eu.max() < 1e-3, (eu.max(), np.percentile(eu, 99.9))
+    if oid != O.MODEL_IALS:
+        np.testing.assert_allclose(loss, lo, rtol=1e-3, atol=1e-6)
+    if oid in (O.MODEL_SAFER2, O.MODEL_CVAR):
+        assert abs(xi - xo) < 1e-4 * max(1.0, abs(xo))
+        np.testing.assert_allclose(dw, wo, rtol=1e-3, atol=1e-5)
+
+
+def _run_model(args, timeout=900):
+    cmd = [os.path.join(BIN, "run_model"), "--train_data", TRAIN, "--test_train_data", VTR,
+           "--test_test_data", VTE, "--seed", "1", "--print_train_stats", "0"] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r.stderr
+
+
+def _ndcg20(log):
+    tail = log[log.rindex("Validation Results"):]
+    m = re.search(r"Mean NDCG@20=([0-9.]+)", tail)
+    assert m, tail[-2000:]
+    return float(m.group(1))
+
+
+def test_gate_ials_run_model():  # ials_test.cc:17-45
+    log = _run_model(["--model_name", "ials", "--dim", "8", "--uobs_weight", "0.1",
+                      "--l2_reg", "0.003", "--epoch", "10"])
+    assert _ndcg20(log) >= 0.2
+    assert len(re.findall(r"Epoch: \d+, Timer: Train=\d+", log)) == 10
+
+
+def test_gate_erm_run_model():  # erm_mf_test.cc:17-45
+    log = _run_model(["--model_name", "ERM_MF", "--dim", "8", "--uobs_weight", "0.004",
+                      "--l2_reg", "0.005", "--epoch", "10"])
+    assert _ndcg20(log) >= 0.2
+
+
+def test_gate_cvar_run_model():  # cvar_mf_test.cc:17-46
+    log = _run_model(["--model_name", "cvar_mf", "--dim", "8", "--uobs_weight", "0.008",
+                      "--l2_reg", "0.002", "--stepsize", "0.4", "--epoch", "50"])
+    assert _ndcg20(log) >= 0.2
+
+
+@pytest.mark.parametrize("epan,bw", [(0, 0.15), (1, 0.7)])
+def test_gate_safer2_run_model(epan, bw):  # safer2_test.cc:17-32, 66-99, 135, 230
+    log = _run_model(["--model_name", "safer2", "--dim", "8", "--uobs_weight", "0.004",
+                      "--l2_reg", "0.004", "--bandwidth", str(bw), "--use_epanechnikov",
+                      str(epan), "--xi_iterations", "5", "--pd_iterations", "1",
+                      "--epoch", "10", "--print_var_stats", "1"])
+    assert _ndcg20(log) >= 0.2
+    means = [float(x) for x in re.findall(r"Min: [0-9.]+, Mean: ([0-9.]+), Max", log)]
+    assert len(means) == 10
+    assert all(abs(m - 0.3) <= 0.02 for m in means), means
+
+
+def test_run_model_rejects_reference_typo():
+    # README's MSD command uses "erm-mf", which the reference CLI rejects too
+    r = subprocess.run([os.path.join(BIN, "run_model"), "--model_name", "erm-mf", "--train_data",
+                        TRAIN, "--test_train_data", VTR, "--test_test_data", VTE],
+                       capture_output=True, text=True)
+    assert r.returncode != 0
