@@ -168,6 +168,16 @@ def main():
     gather_bytes = float(h.sum() * d * 4 + h.sum() * 4 + (n_own + 1) * 8 + n_own * d * 4)
     gather_gbs = gather_bytes / (avg_ms * 1e-3) / 1e9
 
+    traffic = None
+    traffic_src = None
+    pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    if os.path.exists(pmc) and world == 1:
+        try:
+            js = json.load(open(pmc))
+            traffic = js.get("solve_user_traffic_bytes")
+            traffic_src = js.get("source")
+        except Exception:
+            traffic = None
     if rank == 0:
         cpu = None
         if args.cpu_seconds > 0 and world == 1:
@@ -199,7 +209,8 @@ def main():
             "kernel_ms_per_epoch": {k: v[0] / max(K, 1) for k, v in timers.items()},
             "roofline": {"bound": "mfma", "kernel": "solve_tiled_kernel<8> (solve_user)",
                          "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
+                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "avg_launch_ms": avg_ms, "flops_per_launch": flops},
             "gather_roofline": {"bound": "hbm", "achieved": gather_gbs, "peak": PEAK_HBM_GBS,
                                 "unit": "GB/s", "frac": gather_gbs / PEAK_HBM_GBS,
