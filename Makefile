@@ -15,9 +15,10 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 CXXFLAGS := -O3 -std=c++17 -Wall -I include -I $(PKG)/include -pthread
 
-HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/gramian.hip $(CSRC)/loss.hip $(CSRC)/capi.hip
+HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/dual.hip $(CSRC)/spectral.hip $(CSRC)/gramian.hip \
+            $(CSRC)/loss.hip $(CSRC)/capi.hip
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
-HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h include/frecsys_hip.h
+HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h $(CSRC)/chol.h include/frecsys_hip.h
 
 .PHONY: all lib oracle run_model model_dump clean
 all: lib oracle run_model model_dump

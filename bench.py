@@ -157,8 +157,10 @@ def main():
     Dp = fh.padded_dim(d)
     su_ms, su_n = ctx.timing("solve_user")
     si_ms, si_n = ctx.timing("solve_item")
-    timers = {k: ctx.timing(k) for k in ("solve_user", "solve_item", "gramian", "user_loss",
-                                          "allgather", "allreduce")}
+    names = ["solve_user", "solve_item", "gramian", "user_loss", "allgather", "allreduce"]
+    names += [f"{s}.{p}" for s in ("solve_user", "solve_item")
+              for p in ("dspace", "basis", "hspace", "rotate")]
+    timers = {k: ctx.timing(k) for k in names}
     lo, hi = ctx.shard_range(fh.SIDE_USER)
     h = np.diff(up)[lo:hi].astype(np.float64)
     n_own = hi - lo

@@ -164,13 +164,23 @@ int frecsys_user_loss(frecsys_ctx* ctx, int32_t side, float beta, int32_t half,
 int frecsys_synchronize(frecsys_ctx* ctx);
 
 /* ---- profiling hooks (bench.py) ----
- * Kernel time accumulated with HIP events recorded on the library's own
- * stream around each launch of kernel class `what` ("solve_user",
+ * Kernel time accumulated with HIP events recorded on the library's
+ * streams around each launch of kernel class `what` ("solve_user",
  * "solve_item", "solve_eval", "gramian", "user_loss", "allgather",
- * "allreduce") since the last frecsys_timing_reset. */
+ * "allreduce"; per solve also "<solve>.dspace" (d x d solve of the long
+ * histories), "<solve>.basis" (tridiagonalisation of G + rotation of the
+ * other side), "<solve>.hspace" (history-space solve), "<solve>.rotate")
+ * since the last frecsys_timing_reset. */
 int frecsys_timing(const frecsys_ctx* ctx, const char* what, double* total_ms,
                    int64_t* launches);
 int frecsys_timing_reset(frecsys_ctx* ctx);
+
+/* ---- diagnostics (tests) ----
+ * The basis the history-space solve uses for G[side]: G = Q T Q^T with Q
+ * orthogonal (Dp x Dp, row-major) and T tridiagonal (diag[Dp],
+ * sub[Dp]: T(k+1, k), sub[Dp-1] = 0); Dp = frecsys_padded_dim(dim).  No
+ * reference counterpart. */
+int frecsys_debug_basis(frecsys_ctx* ctx, int32_t side, float* q, float* diag, float* sub);
 
 #ifdef __cplusplus
 }

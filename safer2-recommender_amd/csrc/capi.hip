@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -76,6 +77,41 @@ struct frecsys_ctx {
   int64_t err_entity = -1;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::map<std::string, Timer> timers;
+  // history-space (dual) path: a second stream for the concurrent d-space
+  // solve of the long histories, the basis of each side's Gramian, the
+  // rotated copy of each side, and the solved rows in the rotated basis
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  float* q[2] = {nullptr, nullptr};      // Dp x Dp
+  float* tri[2] = {nullptr, nullptr};    // [2 * Dp]: diagonal, subdiagonal
+  float* refl[2] = {nullptr, nullptr};   // Dp x Dp reflectors + [Dp] tau
+  float* xrot[2] = {nullptr, nullptr};   // n_s x Dp
+  float* out_rot[3] = {nullptr, nullptr, nullptr};
+  size_t cap_xrot[2] = {0, 0};
+  size_t cap_out_rot[3] = {0, 0, 0};
+  float* dual_table = nullptr;  // [entities][3][Dp] LDL^T factors
+  size_t cap_dual_table = 0;
+  // long-history split of the d-space solve
+  int split_rows = 1024;         // rows per partial SYRK (FRECSYS_SPLIT_ROWS, 0 = off)
+  std::vector<int2> h_split;
+  std::vector<SplitWork> h_work;
+  int2* d_split = nullptr;
+  size_t cap_split = 0;
+  SplitWork* d_work = nullptr;
+  size_t cap_work = 0;
+  float* d_slabs = nullptr;
+  size_t cap_slabs = 0;
+  std::vector<int32_t> order_h[3];       // history lengths in queue order
+  int dual_on = 1;
+  int dual_max_h = 256;
+  int dual_serial = 0;  // FRECSYS_DUAL_SERIAL=1: no stream overlap (profiling)
+  // per-kernel event pairs, resolved after the call's final synchronisation
+  struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> event_pool;
 };
 
 namespace {
@@ -184,7 +220,76 @@ int build_order(frecsys_ctx* c, int side) {
                                       c->stream) != hipSuccess)
     return fail(c, FRECSYS_ERR_HIP, "hipMemcpy failed (order)");
   c->order_n[side] = (int64_t)recs.size();
+  c->order_h[side].resize(recs.size());
+  for (size_t i = 0; i < recs.size(); ++i) c->order_h[side][i] = recs[i].h;
   c->order_stale[side] = false;
+  return FRECSYS_OK;
+}
+
+// Long-history split of the d-space queue prefix [0, n): entities with
+// more than 2*split_rows assembly rows get their SYRK cut into split_rows
+// slabs done by separate workgroups (launch_split_syrk) before the solve.
+int plan_split(frecsys_ctx* c, const std::vector<int32_t>& hs, int64_t n,
+               const std::function<int64_t(int64_t)>& heff, SolveArgs* a) {
+  a->split = nullptr;
+  a->n_split = 0;
+  a->slabs = nullptr;
+  a->work = nullptr;
+  a->n_work = 0;
+  const int64_t C = c->split_rows;
+  if (C <= 0 || c->Dp < 32) return FRECSYS_OK;
+  c->h_split.clear();
+  c->h_work.clear();
+  int32_t slab = 0;
+  for (int64_t i = 0; i < n && heff(hs[i]) > 2 * C; ++i) {
+    const int64_t ne = heff(hs[i]);
+    const int32_t first = slab;
+    for (int64_t k = 0; k < ne; k += C)
+      c->h_work.push_back(SplitWork{(int32_t)i, (int32_t)k, (int32_t)std::min(ne, k + C), slab++});
+    c->h_split.push_back(int2{first, slab - first});
+  }
+  if (c->h_split.empty()) return FRECSYS_OK;
+  int rc = ensure(c, &c->d_split, &c->cap_split, c->h_split.size());
+  if (rc) return rc;
+  rc = ensure(c, &c->d_work, &c->cap_work, c->h_work.size());
+  if (rc) return rc;
+  rc = ensure(c, &c->d_slabs, &c->cap_slabs, (size_t)slab * split_slab_floats(c->Dp));
+  if (rc) return rc;
+  HIP_TRY(c, hipMemcpy(c->d_split, c->h_split.data(), sizeof(int2) * c->h_split.size(),
+                       hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->d_work, c->h_work.data(), sizeof(SplitWork) * c->h_work.size(),
+                       hipMemcpyHostToDevice));
+  a->split = c->d_split;
+  a->n_split = (int64_t)c->h_split.size();
+  a->slabs = c->d_slabs;
+  a->work = c->d_work;
+  a->n_work = (int64_t)c->h_work.size();
+  return FRECSYS_OK;
+}
+
+// Basis of the other side's Gramian, G = Q T Q^T, and the other side
+// rotated into it (X Q): the inputs of the history-space solve.
+int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
+  const int Dp = c->Dp;
+  size_t cap = 0;
+  if (!c->q[other]) {
+    int rc = ensure(c, &c->q[other], &cap, (size_t)Dp * Dp);
+    if (rc) return rc;
+    cap = 0;
+    rc = ensure(c, &c->tri[other], &cap, (size_t)2 * Dp);
+    if (rc) return rc;
+    cap = 0;
+    rc = ensure(c, &c->refl[other], &cap, (size_t)Dp * Dp + Dp);
+    if (rc) return rc;
+  }
+  int rc = ensure(c, &c->xrot[other], &c->cap_xrot[other],
+                  (size_t)std::max<int64_t>(c->n[other], 1) * Dp);
+  if (rc) return rc;
+  float* tau = c->refl[other] + (size_t)Dp * Dp;
+  HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp, c->refl[other],
+                            tau, s));
+  HIP_TRY(c, launch_form_q(c->refl[other], tau, Dp, c->q[other], s));
+  HIP_TRY(c, launch_rot_gemm(X, nullptr, 0, c->n[other], c->q[other], 0, c->xrot[other], Dp, s));
   return FRECSYS_OK;
 }
 
@@ -229,6 +334,42 @@ struct ScopedTimer {
     }
   }
 };
+
+// Event pair around one launch on any stream; resolved by flush_ktimers
+// after the stream has been synchronised.
+hipEvent_t pool_event(frecsys_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+size_t ktimer_begin(frecsys_ctx* c, const std::string& name, hipStream_t s) {
+  frecsys_ctx::Pending p{name, pool_event(c), pool_event(c)};
+  (void)hipEventRecord(p.a, s);
+  c->pending.push_back(p);
+  return c->pending.size() - 1;
+}
+void ktimer_end(frecsys_ctx* c, size_t i, hipStream_t s) {
+  (void)hipEventRecord(c->pending[i].b, s);
+}
+void flush_ktimers(frecsys_ctx* c) {
+  for (auto& p : c->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess &&
+        hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      Timer& t = c->timers[p.name];
+      t.total_ms += ms;
+      t.launches += 1;
+    }
+    c->event_pool.push_back(p.a);
+    c->event_pool.push_back(p.b);
+  }
+  c->pending.clear();
+}
 
 // Restatement of libstdc++ std::normal_distribution<float>::operator()
 // (Marsaglia polar; bits/random.tcc) over std::generate_canonical<float,24>
@@ -331,6 +472,15 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
     return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed"));
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_HIP, "hipEventCreate failed"));
+  if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed (stream2)"));
+  if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
+  if (const char* v = getenv("FRECSYS_DUAL_MAX_H")) c->dual_max_h = atoi(v);
+  if (const char* v = getenv("FRECSYS_DUAL_SERIAL")) c->dual_serial = atoi(v);
+  if (const char* v = getenv("FRECSYS_SPLIT_ROWS")) c->split_rows = atoi(v);
+  c->dual_max_h = std::min(c->dual_max_h, 32 * kDualMaxTiles);
   for (int s = 0; s < 2; ++s) {
     const size_t rows = (size_t)std::max<int64_t>(c->n[s], 1);
     if (hipMalloc((void**)&c->emb[s], sizeof(float) * rows * Dp) != hipSuccess ||
@@ -371,6 +521,23 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (c->d_counter) (void)hipFree(c->d_counter);
   for (int s = 0; s < 3; ++s)
     if (c->d_order[s]) (void)hipFree(c->d_order[s]);
+  for (int s = 0; s < 2; ++s)
+    for (float* p : {c->q[s], c->tri[s], c->refl[s], c->xrot[s]})
+      if (p) (void)hipFree(p);
+  for (int s = 0; s < 3; ++s)
+    if (c->out_rot[s]) (void)hipFree(c->out_rot[s]);
+  if (c->dual_table) (void)hipFree(c->dual_table);
+  if (c->d_split) (void)hipFree(c->d_split);
+  if (c->d_work) (void)hipFree(c->d_work);
+  if (c->d_slabs) (void)hipFree(c->d_slabs);
+  for (auto& p : c->pending) c->event_pool.insert(c->event_pool.end(), {p.a, p.b});
+  for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->stream2) {
+    (void)hipStreamSynchronize(c->stream2);
+    (void)hipStreamDestroy(c->stream2);
+  }
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -576,7 +743,11 @@ int frecsys_set_gramian(frecsys_ctx* c, int32_t side, const float* host, int64_t
   return FRECSYS_OK;
 }
 
-int frecsys_solve_side(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p) {
+}  // extern "C"
+
+namespace {
+int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
+                    bool force_dspace) {
   if (!c || !valid_side(side) || !p) return fail(c, FRECSYS_ERR_INVALID, "solve: bad arguments");
   if (!c->rp[side]) return fail(c, FRECSYS_ERR_INVALID, "solve: no CSR loaded for side");
   const int kind = p->kind;
@@ -633,16 +804,131 @@ int frecsys_solve_side(frecsys_ctx* c, int32_t side, const frecsys_solve_params*
   a.entity_reg = vkind ? c->d_entity_reg : nullptr;
   a.other_weight = vkind ? c->d_other_weight : nullptr;
   a.fail = c->d_fail;
+  a.split = nullptr;
+  a.n_split = 0;
+  a.slabs = nullptr;
+  a.work = nullptr;
+  a.n_work = 0;
   {
     static const int dbg = getenv("FRECSYS_DEBUG_SKIP") ? atoi(getenv("FRECSYS_DEBUG_SKIP")) : 0;
     a.debug_skip = dbg;
   }
   const unsigned long long none = ~0ull;
   HIP_TRY(c, hipMemcpyAsync(c->d_fail, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
+  // Queue split: the queue is sorted by decreasing history, and h_eff (the
+  // rows the assembly reads, tail-quirk rows included) is monotone in h, so
+  // the d-space entities are a prefix, then the history-space buckets
+  // (32*(t-1) < h_eff <= 32*t, t = 8..1), then the empty histories.
+  const std::vector<int32_t>& hs = c->order_h[side];
+  auto heff = [&](int64_t h) -> int64_t {
+    return (vkind && c->quirks && h > 128 && (h % 128) != 0) ? h + 128 - (h % 128) : h;
+  };
+  auto first_le = [&](int64_t lim) {  // first queue index with h_eff <= lim
+    return (int64_t)(std::partition_point(hs.begin(), hs.end(),
+                                          [&](int32_t h) { return heff(h) > lim; }) -
+                     hs.begin());
+  };
+  // The history-space form needs M = mu*G + lam*I SPD for every entity:
+  // lam > 0 and mu >= 0 (G is PSD).  Otherwise (and when it reports a
+  // non-positive pivot) the call runs the d-space solve for everyone.
+  bool m_spd = p->reg > 0.0f && p->unobserved_weight >= 0.0f;
+  if (m_spd && ukind && p->entity_weight)
+    for (int64_t i = 0; i < c->n[side] && m_spd; ++i) m_spd = p->entity_weight[i] >= 0.0f;
+  if (m_spd && vkind && !p->lambda_is_reg) {
+    const float base = p->alpha * p->unobserved_weight * (float)c->n[other];
+    for (int64_t i = 0; i < c->n[side] && m_spd; ++i) m_spd = p->entity_reg[i] + base > 0.0f;
+  }
+  const bool dual = c->dual_on && !force_dspace && m_spd && !grad && c->Dp >= 64 &&
+                    c->dual_max_h > 0 && (int64_t)hs.size() == c->order_n[side];
+  const int64_t n_dspace = dual ? first_le(c->dual_max_h) : a.n_rows;
+  const int64_t n_nonempty = dual ? first_le(0) : a.n_rows;
   {
     static const char* names[3] = {"solve_user", "solve_item", "solve_eval"};
+    const std::string pre = names[side];
     ScopedTimer t(c, names[side]);
-    HIP_TRY(c, launch_solve(c->Dp, a, c->stream));
+    if (!dual || n_dspace >= n_nonempty) {
+      SolveArgs ap = a;
+      if (c->Dp >= 32 && (int64_t)hs.size() == c->order_n[side]) {
+        rc = plan_split(c, hs, a.n_rows, heff, &ap);
+        if (rc) return rc;
+      }
+      const size_t k = ktimer_begin(c, pre + ".dspace", c->stream);
+      HIP_TRY(c, launch_split_syrk(c->Dp, ap, c->stream));
+      HIP_TRY(c, launch_solve(c->Dp, ap, c->stream));
+      ktimer_end(c, k, c->stream);
+    } else {
+      // d-space solve of the long histories on stream2, concurrently with
+      // the basis change + history-space solve of the rest on stream
+      hipStream_t s2 = c->dual_serial ? c->stream : c->stream2;
+      if (n_dspace > 0) {
+        HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
+        SolveArgs ap = a;
+        ap.n_rows = n_dspace;
+        rc = plan_split(c, hs, n_dspace, heff, &ap);
+        if (rc) return rc;
+        const size_t k = ktimer_begin(c, pre + ".dspace", s2);
+        HIP_TRY(c, launch_split_syrk(c->Dp, ap, s2));
+        HIP_TRY(c, launch_solve(c->Dp, ap, s2));
+        ktimer_end(c, k, s2);
+        HIP_TRY(c, hipEventRecord(c->ev_join, s2));
+      }
+      size_t k = ktimer_begin(c, pre + ".basis", c->stream);
+      rc = prepare_basis(c, other, a.X, c->stream);
+      if (rc) return rc;
+      ktimer_end(c, k, c->stream);
+      rc = ensure(c, &c->out_rot[side], &c->cap_out_rot[side],
+                  (size_t)std::max<int64_t>(c->n[side], 1) * c->Dp);
+      if (rc) return rc;
+      DualArgs d;
+      d.kind = kind;
+      d.quirk = c->quirks;
+      d.Dp = c->Dp;
+      d.col = a.col;
+      d.Xrot = c->xrot[other];
+      d.tdiag = c->tri[other];
+      d.toff = c->tri[other] + c->Dp;
+      d.n_other = a.n_other;
+      d.out_rot = c->out_rot[side];
+      d.reg = a.reg;
+      d.reg_exp = a.reg_exp;
+      d.w = a.w;
+      d.alpha = a.alpha;
+      d.lambda_is_reg = a.lambda_is_reg;
+      d.entity_weight = a.entity_weight;
+      d.entity_reg = a.entity_reg;
+      d.other_weight = a.other_weight;
+      d.fail = a.fail;
+      const int64_t n_hs = n_nonempty - n_dspace;
+      rc = ensure(c, &c->dual_table, &c->cap_dual_table, (size_t)n_hs * 3 * c->Dp);
+      if (rc) return rc;
+      k = ktimer_begin(c, pre + ".hspace", c->stream);
+      d.order = a.order + n_dspace;
+      d.n_rows = n_hs;
+      d.table = c->dual_table;
+      HIP_TRY(c, launch_dual_ldl(d, c->stream));
+      int64_t lo = n_dspace;
+      for (int tiles = kDualMaxTiles; tiles >= 1 && lo < n_nonempty; --tiles) {
+        const int64_t hi = std::min(n_nonempty, first_le(32 * (tiles - 1)));
+        if (hi > lo) {
+          d.order = a.order + lo;
+          d.n_rows = hi - lo;
+          d.table = c->dual_table + (size_t)(lo - n_dspace) * 3 * c->Dp;
+          HIP_TRY(c, launch_dual(tiles, d, c->stream));
+        }
+        lo = std::max(lo, hi);
+      }
+      d.order = a.order + n_dspace;
+      d.n_rows = n_hs;
+      d.table = c->dual_table;
+      HIP_TRY(c, launch_dual_sweep(d, c->stream));
+      ktimer_end(c, k, c->stream);
+      k = ktimer_begin(c, pre + ".rotate", c->stream);
+      HIP_TRY(c, launch_rot_gemm(c->out_rot[side], a.order + n_dspace, 0, n_nonempty - n_dspace,
+                                 c->q[other], 1, a.out, c->Dp, c->stream));
+      ktimer_end(c, k, c->stream);
+      if (n_dspace > 0) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+    }
     t.stop();
   }
   unsigned long long f = none;
@@ -654,12 +940,25 @@ int frecsys_solve_side(frecsys_ctx* c, int32_t side, const frecsys_solve_params*
     t.stop();
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  flush_ktimers(c);
+  if (f != none && dual && n_dspace < n_nonempty) {
+    // a history-space pivot failed: the verdict is the d-space solve's
+    return solve_side_impl(c, side, p, true);
+  }
   if (f != none) {
     c->err_entity = (int64_t)f - 1;
     return fail(c, FRECSYS_ERR_NOT_SPD,
                 "LLT failed (matrix not SPD) for entity " + std::to_string(c->err_entity));
   }
   return FRECSYS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int frecsys_solve_side(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p) {
+  return solve_side_impl(c, side, p, false);
 }
 
 int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, float* host_out) {
@@ -715,6 +1014,24 @@ int frecsys_timing(const frecsys_ctx* c, const char* what, double* total_ms, int
   auto it = c->timers.find(what);
   if (total_ms) *total_ms = it == c->timers.end() ? 0.0 : it->second.total_ms;
   if (launches) *launches = it == c->timers.end() ? 0 : it->second.launches;
+  return FRECSYS_OK;
+}
+
+int frecsys_debug_basis(frecsys_ctx* c, int32_t side, float* q, float* diag, float* sub) {
+  if (!c || side < 0 || side > 1 || !q || !diag || !sub)
+    return fail(c, FRECSYS_ERR_INVALID, "debug_basis: bad arguments");
+  if (c->Dp < 64) return fail(c, FRECSYS_ERR_UNSUPPORTED, "debug_basis: Dp < 64");
+  HIP_TRY(c, hipSetDevice(c->device));
+  int rc = prepare_basis(c, side, c->emb[side], c->stream);
+  if (rc) return rc;
+  const size_t Dp = (size_t)c->Dp;
+  HIP_TRY(c, hipMemcpyAsync(q, c->q[side], sizeof(float) * Dp * Dp, hipMemcpyDeviceToHost,
+                            c->stream));
+  HIP_TRY(c, hipMemcpyAsync(diag, c->tri[side], sizeof(float) * Dp, hipMemcpyDeviceToHost,
+                            c->stream));
+  HIP_TRY(c, hipMemcpyAsync(sub, c->tri[side] + Dp, sizeof(float) * Dp, hipMemcpyDeviceToHost,
+                            c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FRECSYS_OK;
 }
 

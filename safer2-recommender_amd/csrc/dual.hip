@@ -1,0 +1,422 @@
+// dual.hip -- history-space solve for short-history entities on gfx950.
+//
+// Same result as the d-space solve (solve.hip; reference Project /
+// ProjectU / ProjectV, ials.h:88-144, safer2.h:104-221) for entities whose
+// history (plus tail-quirk rows) h_eff is at most 32 * kDualMaxTiles, at a
+// fraction of the work when h_eff < d.  Write the normal matrix as
+//   A = M + Xt^T Xt,  M = mu*G + lam*I,  b = Xt^T s
+// (Xt: history rows times c_j = sqrt of their weight in A; s_j = c_j for
+// real rows, 0 for the rows the ProjectV tail quirk adds to A only).
+// Push-through: x = M^-1 Xt^T (I + Xt M^-1 Xt^T)^-1 s.  In the basis of
+// G = Q T Q^T (spectral.hip) M = Q (mu*T + lam*I) Q^T, and with the LDL^T
+// factorisation mu*T + lam*I = L D L^T (L unit lower bidiagonal):
+//   Z = Y L^-T  (Y = Xt Q: gathered rows of the pre-rotated other side),
+//   S = I + Z D^-1 Z^T              h_p x h_p, MFMA SYRK over k = 0..Dp-1
+//   z = S^-1 s                       blocked Cholesky in LDS (chol.h)
+//   x' = L^-T D^-1 L^-1 (Y^T z)     two bidiagonal sweeps
+// and x = Q x' is applied to all rows of the launch by rot_gemm afterwards.
+//
+// Three kernels per half-step (plus the basis change, spectral.hip):
+//   dual_ldl_kernel    one thread per entity: LDL^T of its tridiagonal
+//                      mu*T + lam*I into a [3][Dp] table row (the serial
+//                      chains run entity-parallel instead of per workgroup);
+//   dual_solve_kernel  one workgroup per entity (below), writes Y^T (c.*z);
+//   dual_sweep_kernel  one thread per entity: x' = L^-T D^-1 L^-1 (Y^T c.*z).
+// dual_solve_kernel, per workgroup (one entity, NW waves):
+//   * the entity's l_k and D^-1/2 come from its table row;
+//   * per slab (32 columns of the h_p rows, staged in LDS with a padded
+//     row stride): each row's lane runs the bidiagonal recurrence
+//     z_j[k] = y_j[k] - l_k z_j[k-1] across the slab (carry in a register)
+//     and writes D^-1/2-scaled values k-major; the waves then accumulate
+//     their S tiles with v_mfma_f32_32x32x2_f32 while the next slab's loads
+//     are in flight;
+//   * S tiles go to LDS (aliasing the slab buffers), chol_solve_tiles, then
+//     Y^T (c.*z) re-reads the (cache-resident) rows with float4 loads.
+#include <hip/hip_runtime.h>
+
+#include "chol.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace frecsys_hip {
+
+namespace {
+
+constexpr int kMaxDp = 256;
+
+template <int TH>
+struct DualCfg {
+  static constexpr int HP = 32 * TH;                // padded history rows
+  static constexpr int NT = TH * (TH + 1) / 2;      // lower tiles of S
+  static constexpr int NW = (TH <= 2) ? 4 : 8;
+  static constexpr int NTHR = NW * 64;
+  static constexpr int MT = (NT + NW - 1) / NW;
+  static constexpr int SROW = 33;                   // slab row stride
+  static constexpr int STG = HP * SROW;
+  static constexpr int ZS = 32 * HP;                // k-major scaled Z slab
+  static constexpr int TILES = NT * 1024;
+  static constexpr int LOOP = ((STG + ZS + 3) / 4) * 4;
+  static constexpr int REGION0 = TILES > LOOP ? TILES : LOOP;
+  static constexpr int OFF_L = REGION0;             // l_k
+  static constexpr int OFF_DS = OFF_L + kMaxDp;     // D^-1/2
+  static constexpr int OFF_C = OFF_DS + kMaxDp;     // c_j
+  static constexpr int OFF_ID = OFF_C + HP;         // row ids
+  static constexpr int OFF_B = OFF_ID + HP;         // s, then y
+  static constexpr int OFF_X = OFF_B + HP;          // z
+  static constexpr int PART = NTHR > NW * 32 ? NTHR : NW * 32;
+  static constexpr int OFF_PART = OFF_X + HP;
+  static constexpr int OFF_FLAG = OFF_PART + PART;
+  static constexpr int TOTAL = OFF_FLAG + 4;
+  static constexpr size_t BYTES = (size_t)TOTAL * 4;
+  static constexpr int NQ = (HP * 8 + NTHR - 1) / NTHR;  // float4 per thread per slab
+  static_assert(BYTES <= 163840, "LDS budget");
+};
+
+__device__ __forceinline__ int64_t virt_pos_d(int64_t k, int64_t h) {
+  return k < h ? k : (h - 128 + (k - h));
+}
+
+// mu, lambda and omega of one entity (see the file comment): iALS
+// lambda from RegularizationValue (ials.h:310-315), ProjectU
+// omega = entity weight (safer2.h:146-147), ProjectV item_reg_.
+__device__ __forceinline__ void dual_scalars(const DualArgs& a, int64_t e, int64_t h, float& mu,
+                                             float& lam, float& omega) {
+  const int kind = a.kind;
+  const bool uk = is_u_kind(kind);
+  omega = (uk && a.entity_weight) ? a.entity_weight[e] : 1.0f;
+  lam = entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other, a.entity_reg, e,
+                      a.lambda_is_reg);
+  mu = uk ? omega * a.w : a.w;
+}
+
+__global__ void __launch_bounds__(256) dual_ldl_kernel(DualArgs a) {
+  __shared__ float td[kMaxDp], to[kMaxDp];
+  const int Dp = a.Dp, tid = threadIdx.x;
+  for (int k = tid; k < Dp; k += 256) {
+    td[k] = a.tdiag[k];
+    to[k] = a.toff[k];
+  }
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * 256 + tid;
+  if (p >= a.n_rows) return;
+  const QueueRec rec = a.order[p];
+  float mu, lam, omega;
+  dual_scalars(a, rec.entity, rec.h, mu, lam, omega);
+  float* lrow = a.table + p * 3 * Dp;
+  float* srow = lrow + Dp;
+  float* irow = srow + Dp;
+  // l_k = b_k / d_{k-1}, d_k = a_k - l_k b_k (a = mu*diag + lam, b = mu*sub);
+  // stored by float4 (the rows of neighbouring lanes are 3*Dp floats apart)
+  float dprev = 1.0f, r = 0.0f;
+  bool ok = true;
+  for (int k4 = 0; k4 < Dp; k4 += 4) {
+    float lv[4], sv[4], iv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k4 + u;
+      const float b = k > 0 ? mu * to[k - 1] : 0.0f;
+      const float l = b * r;
+      const float dk = (mu * td[k] + lam) - l * b;
+      ok = ok && (dk > 0.0f);
+      r = __builtin_amdgcn_rcpf(dk);
+      lv[u] = l;
+      sv[u] = __builtin_amdgcn_rsqf(dk);
+      iv[u] = r;
+      dprev = dk;
+    }
+    *reinterpret_cast<float4*>(lrow + k4) = make_float4(lv[0], lv[1], lv[2], lv[3]);
+    *reinterpret_cast<float4*>(srow + k4) = make_float4(sv[0], sv[1], sv[2], sv[3]);
+    *reinterpret_cast<float4*>(irow + k4) = make_float4(iv[0], iv[1], iv[2], iv[3]);
+  }
+  (void)dprev;
+  if (!ok) atomicMin(a.fail, (unsigned long long)(rec.entity + 1));
+}
+
+// x' = L^-T D^-1 L^-1 v, in place on the entity's out_rot row.
+__global__ void __launch_bounds__(256) dual_sweep_kernel(DualArgs a) {
+  const int Dp = a.Dp;
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= a.n_rows) return;
+  const int64_t e = a.order[p].entity;
+  float* v = a.out_rot + e * Dp;
+  const float* lrow = a.table + p * 3 * Dp;
+  const float* irow = lrow + 2 * Dp;
+  float u = 0.0f;
+  for (int k4 = 0; k4 < Dp; k4 += 4) {  // L u = v, then D^-1
+    float4 vv = *reinterpret_cast<const float4*>(v + k4);
+    const float4 ll = *reinterpret_cast<const float4*>(lrow + k4);
+    const float4 ii = *reinterpret_cast<const float4*>(irow + k4);
+    u = vv.x - ll.x * u;
+    vv.x = u * ii.x;
+    u = vv.y - ll.y * u;
+    vv.y = u * ii.y;
+    u = vv.z - ll.z * u;
+    vv.z = u * ii.z;
+    u = vv.w - ll.w * u;
+    vv.w = u * ii.w;
+    *reinterpret_cast<float4*>(v + k4) = vv;
+  }
+  float x = 0.0f, lnext = 0.0f;  // L^T x = D^-1 u, l_Dp = 0
+  for (int k4 = Dp - 4; k4 >= 0; k4 -= 4) {
+    float4 ww = *reinterpret_cast<const float4*>(v + k4);
+    const float4 ll = *reinterpret_cast<const float4*>(lrow + k4);
+    x = ww.w - lnext * x;
+    ww.w = x;
+    x = ww.z - ll.w * x;
+    ww.z = x;
+    x = ww.y - ll.z * x;
+    ww.y = x;
+    x = ww.x - ll.y * x;
+    ww.x = x;
+    lnext = ll.x;
+    *reinterpret_cast<float4*>(v + k4) = ww;
+  }
+}
+
+template <int TH>
+__global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs a) {
+  using C = DualCfg<TH>;
+  constexpr int HP = C::HP, NT = C::NT, NW = C::NW, NTHR = C::NTHR, MT = C::MT;
+  constexpr int SROW = C::SROW, NQ = C::NQ;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* tiles = smem;
+  float* stage = smem;
+  float* zs = smem + C::STG;
+  float* lsub = smem + C::OFF_L;
+  float* dsq = smem + C::OFF_DS;
+  float* cvec = smem + C::OFF_C;
+  int* ids = reinterpret_cast<int*>(smem + C::OFF_ID);
+  float* bvec = smem + C::OFF_B;
+  float* xvec = smem + C::OFF_X;
+  float* part = smem + C::OFF_PART;
+  int* flag = reinterpret_cast<int*>(smem + C::OFF_FLAG);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lo = lane & 31, hi = lane >> 5;
+  const int kind = a.kind;
+  const bool vk = is_v_kind(kind), uk = is_u_kind(kind);
+  const int Dp = a.Dp, NC = Dp >> 5;
+
+  const QueueRec rec = a.order[blockIdx.x];
+  const int64_t e = rec.entity;
+  const int64_t h = rec.h;
+  const int64_t p0 = rec.p0;
+  int64_t extra = 0;
+  if (vk && a.quirk && h > 128 && (h % 128) != 0) extra = 128 - (h % 128);
+  const int ntot = (int)(h + extra);  // <= HP (host bucketing)
+
+  const float hf = (float)h;
+  float mu, lam, omega;
+  dual_scalars(a, e, h, mu, lam, omega);
+  (void)mu;
+  (void)lam;
+
+  if (tid < HP) {
+    int id = -1;
+    float cj = 0.0f;
+    if (tid < ntot) {
+      id = a.col[p0 + virt_pos_d(tid, h)];
+      // weights of the row in A (= in b): iALS 1 (ials.h:122-126), ProjectU
+      // omega/h (safer2.h:143-147), ProjectV nu (safer2.h:185-192)
+      cj = vk ? sqrtf(a.other_weight[id]) : (uk ? sqrtf(omega / hf) : 1.0f);
+    }
+    ids[tid] = id;
+    cvec[tid] = cj;
+    bvec[tid] = tid < h ? cj : 0.0f;
+  }
+  if (tid == 0) flag[0] = 0;
+  {  // l_k and D^-1/2 from the entity's table row
+    const float* trow = a.table + (int64_t)blockIdx.x * 3 * Dp;
+    for (int k = tid; k < Dp; k += NTHR) {
+      lsub[k] = trow[k];
+      dsq[k] = trow[Dp + k];
+    }
+  }
+  __syncthreads();
+
+  float4 regs[NQ];
+  auto load_slab = [&](int c) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int s = tid + q * NTHR;
+      regs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if ((HP * 8) % NTHR == 0 || s < HP * 8) {
+        const int r = s >> 3, c4 = s & 7;
+        const int id = ids[r];
+        if (id >= 0)
+          regs[q] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)id * Dp + 32 * c + 4 * c4);
+      }
+    }
+  };
+  auto store_slab = [&]() {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int s = tid + q * NTHR;
+      if ((HP * 8) % NTHR == 0 || s < HP * 8) {
+        const int r = s >> 3, c4 = s & 7;
+        float* d = stage + r * SROW + 4 * c4;
+        d[0] = regs[q].x;
+        d[1] = regs[q].y;
+        d[2] = regs[q].z;
+        d[3] = regs[q].w;
+      }
+    }
+  };
+
+  load_slab(0);
+  store_slab();
+  __syncthreads();
+
+  // ---- S = Z D^-1 Z^T accumulated over the 32-column slabs ----
+  f32x16 acc[MT];
+  int aoff[MT], boff[MT];
+  bool valid[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int t = wave + m * NW;
+    valid[m] = t < NT;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    aoff[m] = 32 * I + lo;
+    boff[m] = 32 * J + lo;
+    acc[m] = f32x16{0.f};
+  }
+  float carry = 0.0f;
+  const float cj = tid < HP ? cvec[tid] : 0.0f;
+  for (int c = 0; c < NC; ++c) {
+    const bool more = c + 1 < NC;
+    if (more) load_slab(c + 1);
+    if (tid < HP) {
+      const float* yrow = stage + tid * SROW;
+      float y[32];
+#pragma unroll
+      for (int kk = 0; kk < 32; ++kk) y[kk] = yrow[kk];
+      float z = carry;
+#pragma unroll
+      for (int kk = 0; kk < 32; ++kk) {
+        const int k = 32 * c + kk;
+        z = y[kk] - lsub[k] * z;
+        zs[kk * HP + tid] = (cj * z) * dsq[k];
+      }
+      carry = z;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int s = 0; s < 16; ++s) {
+      const float* zr = zs + (2 * s + hi) * HP;
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        if (valid[m]) acc[m] = mfma32(zr[aoff[m]], zr[boff[m]], acc[m]);
+    }
+    if (more) store_slab();
+    __syncthreads();
+  }
+
+  // ---- S = I + acc into the swizzled LDS tiles (aliasing the slabs) ----
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    if (valid[m]) {
+      const int I = (aoff[m] - lo) >> 5, J = (boff[m] - lo) >> 5;
+      float* tile = tiles + tidx(I, J) * 1024;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = acc_row(q, hi);
+        const bool dg = (32 * I + i) == (32 * J + lo);
+        tile[sw(i, lo)] = acc[m][q] + (dg ? 1.0f : 0.0f);
+      }
+    }
+  }
+  __syncthreads();
+  chol_solve_tiles<TH, NW>(tiles, bvec, xvec, part, flag, tid, 0);
+
+  // ---- v = Y^T (c.*z): the rows again, float4 per lane, 8 rows in flight ----
+  {
+    const int D4 = Dp >> 2, R = NTHR / D4;  // column quads x row groups
+    const int c4 = tid % D4, g = tid / D4;
+    float* red = tiles;  // the S tiles are dead after the solve
+    float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g < R) {
+      for (int j0 = g; j0 < ntot; j0 += 8 * R) {
+        float4 rv[8];
+        float wv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = j0 + u * R;
+          rv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          wv[u] = 0.0f;
+          if (j < ntot) {
+            wv[u] = cvec[j] * xvec[j];
+            rv[u] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)ids[j] * Dp + 4 * c4);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          acc4.x += wv[u] * rv[u].x;
+          acc4.y += wv[u] * rv[u].y;
+          acc4.z += wv[u] * rv[u].z;
+          acc4.w += wv[u] * rv[u].w;
+        }
+      }
+      *reinterpret_cast<float4*>(red + g * Dp + 4 * c4) = acc4;
+    }
+    __syncthreads();
+    if (tid < Dp) {
+      float v = 0.0f;
+      for (int gg = 0; gg < R; ++gg) v += red[gg * Dp + tid];
+      a.out_rot[e * Dp + tid] = v;
+    }
+  }
+  if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
+}
+
+template <int TH>
+hipError_t launch_dual_t(const DualArgs& a, hipStream_t s) {
+  using C = DualCfg<TH>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t err = hipFuncSetAttribute((const void*)dual_solve_kernel<TH>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)C::BYTES);
+    if (err != hipSuccess) return err;
+    attr = true;
+  }
+  hipLaunchKernelGGL(dual_solve_kernel<TH>, dim3((unsigned)a.n_rows), dim3(C::NTHR), C::BYTES, s,
+                     a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_dual_ldl(const DualArgs& a, hipStream_t s) {
+  if (a.n_rows <= 0) return hipSuccess;
+  if (a.Dp < 64 || a.Dp > kMaxDp || (a.Dp & 31)) return hipErrorInvalidValue;
+  const unsigned nb = (unsigned)((a.n_rows + 255) / 256);
+  hipLaunchKernelGGL(dual_ldl_kernel, dim3(nb), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dual_sweep(const DualArgs& a, hipStream_t s) {
+  if (a.n_rows <= 0) return hipSuccess;
+  const unsigned nb = (unsigned)((a.n_rows + 255) / 256);
+  hipLaunchKernelGGL(dual_sweep_kernel, dim3(nb), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_dual(int tiles, const DualArgs& a, hipStream_t s) {
+  if (a.n_rows <= 0) return hipSuccess;
+  if (a.Dp < 64 || a.Dp > kMaxDp || (a.Dp & 31)) return hipErrorInvalidValue;
+  switch (tiles) {
+    case 1: return launch_dual_t<1>(a, s);
+    case 2: return launch_dual_t<2>(a, s);
+    case 3: return launch_dual_t<3>(a, s);
+    case 4: return launch_dual_t<4>(a, s);
+    case 5: return launch_dual_t<5>(a, s);
+    case 6: return launch_dual_t<6>(a, s);
+    case 7: return launch_dual_t<7>(a, s);
+    case 8: return launch_dual_t<8>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace frecsys_hip

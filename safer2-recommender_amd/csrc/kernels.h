@@ -15,6 +15,15 @@ struct QueueRec {
   int64_t p0;
 };
 
+// One partial SYRK of a long history: queue position, virtual history
+// positions [k0, k1), output slab.
+struct SplitWork {
+  int32_t pos;
+  int32_t k0;
+  int32_t k1;
+  int32_t slab;
+};
+
 // Everything one launch of the per-entity solve needs (device pointers).
 struct SolveArgs {
   int kind;                 // FRECSYS_KIND_*
@@ -37,6 +46,12 @@ struct SolveArgs {
   const float* other_weight;   // [rows of other side] nu
   unsigned long long* fail;    // atomicMin(entity + 1) on a non-SPD pivot
   int debug_skip;              // diagnostic ablation mask (0 in production)
+  // long-history split (tiled kernel only; nullptr / 0 = none)
+  const int2* split;           // [n_split] per queue position: first slab, slab count
+  int64_t n_split;
+  float* slabs;                // [slabs][split_slab_floats(Dp)]
+  const SplitWork* work;       // [n_work] partial SYRK items
+  int64_t n_work;
 };
 
 struct GramArgs {
@@ -65,7 +80,60 @@ int64_t gram_num_blocks(int Dp, int64_t n);
 // Partial workspace floats needed for n rows at padded dim Dp.
 size_t gram_workspace_floats(int Dp, int64_t n);
 
+// History-space ("dual") solve of the short-history entities (dual.hip).
+// With G = Q T Q^T (Q orthogonal, T tridiagonal) and M = mu*G + lam*I,
+// A = M + Xt^T Xt, b = Xt^T s  (Xt = the history rows scaled by sqrt of
+// their A-weight, s = the matching rhs coefficients) is solved as
+//   x = Q (mu*T + lam*I)^-1 Y^T z,  z = (I + Y (mu*T + lam*I)^-1 Y^T)^-1 s,
+// Y = Xt Q (push-through identity): an h x h SPD system instead of d x d.
+struct DualArgs {
+  int kind;                 // FRECSYS_KIND_IALS / WEIGHTED_U / WEIGHTED_V
+  int quirk;
+  int Dp;
+  const QueueRec* order;    // [n_rows] this launch's entities
+  int64_t n_rows;
+  const int32_t* col;       // CSR columns of the solved side
+  const float* Xrot;        // other side rotated into the T basis: X Q, ld Dp
+  const float* tdiag;       // [Dp] diagonal of T
+  const float* toff;        // [Dp] T(k+1, k)
+  int64_t n_other;
+  float* out_rot;           // Y^T z per solved row (row = entity), ld Dp
+  float* table;             // [n_rows][3][Dp]: l_k, D^-1/2, D^-1 of mu*T + lam*I
+  float reg, reg_exp, w, alpha;
+  int lambda_is_reg;
+  const float* entity_weight;
+  const float* entity_reg;
+  const float* other_weight;
+  unsigned long long* fail;
+};
+
+// Largest history-space tile count built (h_eff <= 32 * kDualMaxTiles).
+constexpr int kDualMaxTiles = 8;
+
 hipError_t launch_solve(int Dp, const SolveArgs& a, hipStream_t s);
+// Partial SYRKs of the split entities (a.work[0..n_work)) into a.slabs.
+hipError_t launch_split_syrk(int Dp, const SolveArgs& a, hipStream_t s);
+size_t split_slab_floats(int Dp);
+// LDL^T of every entity's tridiagonal mu*T + lam*I (one thread per entity,
+// a.order[0..n_rows)) into a.table.
+hipError_t launch_dual_ldl(const DualArgs& a, hipStream_t s);
+// out_rot rows of a.order[0..n_rows): v -> L^-T D^-1 L^-1 v (one thread per
+// entity, table rows as written by launch_dual_ldl).
+hipError_t launch_dual_sweep(const DualArgs& a, hipStream_t s);
+// One launch per history bucket: every entity of a.order has
+// 32*(tiles-1) < h_eff <= 32*tiles.
+hipError_t launch_dual(int tiles, const DualArgs& a, hipStream_t s);
+// Householder tridiagonalisation G = Q T Q^T of a Dp x Dp symmetric matrix
+// (one workgroup): T's diagonal / subdiagonal, the reflectors (row k of Vh,
+// entries k+1..Dp-1) and their tau.
+hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
+                          float* tau, hipStream_t s);
+// Q = H_0 H_1 ... H_{Dp-3} from the reflectors, row-major Dp x Dp.
+hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s);
+// Y[row] = X[row] * (trans ? Q^T : Q) for rows r0..r0+n-1, or for the
+// entities rows[0..n) when rows != nullptr.  X, Y: ld Dp.
+hipError_t launch_rot_gemm(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
+                           const float* Q, int trans, float* Y, int Dp, hipStream_t s);
 hipError_t launch_gramian(int Dp, const GramArgs& a, hipStream_t s);
 hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s);
 hipError_t launch_zero_gram(int Dp, float* G, hipStream_t s);

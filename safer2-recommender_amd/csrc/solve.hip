@@ -30,6 +30,7 @@
 // solve by one lane (the reference's own tests run at dim 8).
 #include <hip/hip_runtime.h>
 
+#include "chol.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -73,65 +74,14 @@ __device__ __forceinline__ int64_t virt_pos(int64_t k, int64_t h) {
   return k < h ? k : (h - 128 + (k - h));
 }
 
-// ---------------------------------------------------------------------
-// 32x32 diagonal block: Cholesky factor AND its inverse by one wave.
-//
-// Lanes 0..31 own row r of A (becoming row r of L); lanes 32..63 own column
-// j = lane-32 of the identity (becoming column j of L^-1).  Both halves run
-// the same left-looking update at step k,
-//     t = a[k] - sum_{m<k} a[m] * L[k][m],
-// which for a row of A is the Cholesky update and for a column of the
-// identity is forward substitution L x = e_j; then a[k] = t / L[k][k] (lane
-// k itself takes the pivot sqrt).  Row k of L (lane k's registers) reaches
-// every lane by v_readlane -- no LDS round trip on the serial chain; the dot
-// product runs in 4 partial chains.  On return L^-1 (lower, upper zeroed)
-// is in the swizzled tile.
-// ---------------------------------------------------------------------
-__device__ __forceinline__ float rdlane(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
-__device__ __forceinline__ bool diag_factor_inv(float* tile, int lane) {
-  const int r = lane & 31;
-  const bool fl = lane < 32;
-  float a[32];
-#pragma unroll
-  for (int c = 0; c < 32; ++c) a[c] = fl ? tile[sw(r, c)] : (c == r ? 1.0f : 0.0f);
-  bool ok = true;
-#pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
-#pragma unroll
-    for (int m = 0; m < k; m += 4) {
-      p0 += a[m] * rdlane(a[m], k);
-      if (m + 1 < k) p1 += a[m + 1] * rdlane(a[m + 1], k);
-      if (m + 2 < k) p2 += a[m + 2] * rdlane(a[m + 2], k);
-      if (m + 3 < k) p3 += a[m + 3] * rdlane(a[m + 3], k);
-    }
-    const float t = a[k] - ((p0 + p1) + (p2 + p3));
-    const float piv = rdlane(t, k);
-    ok = ok && (piv > 0.0f);
-    const float d = sqrtf(piv);
-    const float rd = 1.0f / d;
-    a[k] = (lane == k) ? d : t * rd;
-  }
-  if (!fl) {  // column j of L^-1 -> tile element (k, j), k >= j
-    const int j = r;
-#pragma unroll
-    for (int k = 0; k < 32; ++k) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
-  }
-  return ok;
-}
-
-// One 32x32 MFMA product u = P Q^T of two LDS tiles (P, Q swizzled).
-__device__ __forceinline__ f32x16 tile_pqT(const float* P, const float* Q, int lo, int hi) {
-  f32x16 u = f32x16{0.f};
-#pragma unroll
-  for (int s = 0; s < 16; ++s) u = mfma32(P[sw(lo, 2 * s + hi)], Q[sw(lo, 2 * s + hi)], u);
-  return u;
-}
-
-template <int T>
+// PARTIAL = true: one workgroup per SplitWork item accumulates the SYRK of
+// the history positions [k0, k1) of a long entity (and its rhs part) and
+// writes the raw accumulators to a workspace slab (register layout: tile t,
+// element (q, lane) at t*1024 + q*64 + lane; rhs at NT*1024).  The entity's
+// own workgroup (PARTIAL = false, a.split[pos].y > 0) then starts from the
+// sum of its slabs instead of gathering -- the longest histories (55K rows
+// on the ML-20M item side) no longer serialise on one CU.
+template <int T, bool PARTIAL>
 __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     solve_tiled_kernel(SolveArgs a) {
   using C = TiledCfg<T>;
@@ -154,7 +104,21 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
   const bool vk = is_v_kind(kind);
 
   // ---- one entity per workgroup, dispatched in LPT order (longest first) ----
-  const QueueRec rec = a.order[blockIdx.x];
+  int qpos = blockIdx.x;
+  int64_t k0 = 0, k1 = 0;
+  int slab0 = 0, nslab = 0;
+  if (PARTIAL) {
+    const SplitWork wk = a.work[blockIdx.x];
+    qpos = wk.pos;
+    k0 = wk.k0;
+    k1 = wk.k1;
+    slab0 = wk.slab;
+  } else if (qpos < a.n_split) {
+    const int2 sp = a.split[qpos];
+    slab0 = sp.x;
+    nslab = sp.y;
+  }
+  const QueueRec rec = a.order[qpos];
   const int64_t e = rec.entity;
   const int64_t h = rec.h;
   const int64_t p0 = rec.p0;
@@ -162,14 +126,15 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
   int64_t extra = 0;
   if (vk && a.quirk && h > 128 && (h % 128) != 0) extra = 128 - (h % 128);
   const int64_t ntot = h + extra;
-  const int nchunks = (int)((ntot + R - 1) / R);
+  if (!PARTIAL) k1 = nslab > 0 ? 0 : ntot;  // split: the slabs hold the rows
+  const int nchunks = (int)((k1 - k0 + R - 1) / R);
 
   auto ring_load = [&](int c, int& id, float& sa, float& bw) {
-    const int64_t k = (int64_t)c * R + tid;
+    const int64_t k = k0 + (int64_t)c * R + tid;
     id = -1;
     sa = 0.0f;
     bw = 0.0f;
-    if (k < ntot) {
+    if (k < k1) {
       id = a.col[p0 + virt_pos(k, h)];
       if (vk) {
         const float nu = a.other_weight[id];
@@ -211,7 +176,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
   };
 
   if (tid == 0) flag[0] = 0;
-  if (tid < R) {
+  if (tid < R && nchunks > 0) {
     int id;
     float sa, bw;
     ring_load(0, id, sa, bw);
@@ -221,7 +186,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
       ring_store(1, id, sa, bw);
     }
   }
-  if (is_grad_kind(kind) && tid < Dp) xvec[tid] = a.E[e * Dp + tid];
+  if (!PARTIAL && is_grad_kind(kind) && tid < Dp) xvec[tid] = a.E[e * Dp + tid];
 
   // ---- my tiles; accumulators start from the G part of A ----
   // (the G reads overlap the history gather that starts below)
@@ -249,7 +214,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     aoff[m] = 32 * I + lo;
     boff[m] = 32 * J + lo;
     acc[m] = f32x16{0.f};
-    if (valid[m] && !grad) {
+    if (!PARTIAL && valid[m] && !grad) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int gi = 32 * I + acc_row(q, hi), gj = 32 * J + lo;
@@ -259,11 +224,27 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
       }
     }
   }
-  __syncthreads();
-  load_data(0);
-  store_stage(0);
-  __syncthreads();
+  // split entity: add its slabs in slab order (deterministic)
   float bacc = 0.0f;
+  const size_t slab_floats = (size_t)NT * 1024 + Dp;
+  for (int sidx = 0; sidx < nslab; ++sidx) {
+    const float* sl = a.slabs + (size_t)(slab0 + sidx) * slab_floats;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (valid[m]) {
+        const int t = wave + m * NW;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[m][q] += sl[t * 1024 + q * 64 + lane];
+      }
+    }
+    if (tid < Dp) bacc += sl[NT * 1024 + tid];
+  }
+  __syncthreads();
+  if (nchunks > 0) {
+    load_data(0);
+    store_stage(0);
+  }
+  __syncthreads();
 
   for (int c = 0; c < nchunks; ++c) {
     const int buf = c & 1;
@@ -299,6 +280,20 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     if (more) store_stage(buf ^ 1);
     if (ring_more) ring_store(c + 2, nid, nsa, nbw);
     __syncthreads();
+  }
+
+  if (PARTIAL) {
+    float* sl = a.slabs + (size_t)slab0 * slab_floats;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (valid[m]) {
+        const int t = wave + m * NW;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) sl[t * 1024 + q * 64 + lane] = acc[m][q];
+      }
+    }
+    if (tid < Dp) sl[NT * 1024 + tid] = bacc;
+    return;
   }
 
   // ---- epilogue: finish A into the swizzled LDS tiles ----
@@ -346,99 +341,8 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     return;
   }
 
-  // ---- blocked right-looking Cholesky with lookahead ----
-  // Diagonal tiles become L_pp^-1.  Wave 0 updates tile (p+1, p+1) first
-  // and factors it while the other waves finish panel p's trailing update.
-  if (wave == 0 && !(a.debug_skip & 2)) {
-    if (!diag_factor_inv(tiles, lane) && lane == 0) flag[0] = 1;
-  }
-  __syncthreads();
-  for (int p = 0; p < T; ++p) {
-    const float* Tpp = tiles + tidx(p, p) * 1024;
-    const int npan = T - 1 - p;
-    // TRSM by MFMA: L_Ip = A_Ip (L_pp^-1)^T ; y_p = L_pp^-1 b_p
-    if (!(a.debug_skip & 4)) {
-      for (int t = wave; t < npan; t += NW) {
-        float* Aip = tiles + tidx(p + 1 + t, p) * 1024;
-        const f32x16 u = tile_pqT(Aip, Tpp, lo, hi);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) Aip[sw(acc_row(q, hi), lo)] = u[q];
-      }
-      if (wave == (npan % NW) && hi == 0) {
-        float y = 0.0f;
-#pragma unroll 8
-        for (int k = 0; k < 32; ++k) y += Tpp[sw(lo, k)] * bvec[32 * p + k];
-        xvec[lo] = y;  // staged; copied into bvec after the barrier
-      }
-    }
-    __syncthreads();
-    if (tid < 32) bvec[32 * p + tid] = xvec[tid];
-    if (p < T - 1) {
-      const int nb = 32 * npan;
-      if (tid >= 64 && tid < 64 + nb) {  // b_J -= L_Jp y_p (y_p still in xvec)
-        const int t2 = tid - 64;
-        const int J = p + 1 + (t2 >> 5), r = t2 & 31;
-        const float* L = tiles + tidx(J, p) * 1024;
-        float t = 0.0f;
-#pragma unroll 8
-        for (int k = 0; k < 32; ++k) t += L[sw(r, k)] * xvec[k];
-        bvec[32 * J + r] -= t;
-      }
-      // trailing update A_IJ -= L_Ip L_Jp^T; tile (p+1, p+1) is index 0
-      const int ntr = npan * (npan + 1) / 2;
-      if (wave == 0) {
-        float* A11 = tiles + tidx(p + 1, p + 1) * 1024;
-        const float* L1 = tiles + tidx(p + 1, p) * 1024;
-        if (!(a.debug_skip & 8)) {
-          const f32x16 u = tile_pqT(L1, L1, lo, hi);
-#pragma unroll
-          for (int q = 0; q < 16; ++q) A11[sw(acc_row(q, hi), lo)] -= u[q];
-        }
-        if (!(a.debug_skip & 2)) {
-          if (!diag_factor_inv(A11, lane) && lane == 0) flag[0] = 1;
-        }
-      } else {
-        for (int tt = wave; tt < ntr && !(a.debug_skip & 8); tt += NW - 1) {
-          int Ir = 0;
-          while ((Ir + 1) * (Ir + 2) / 2 <= tt) ++Ir;
-          const int Jr = tt - Ir * (Ir + 1) / 2;
-          const int I = p + 1 + Ir, J = p + 1 + Jr;
-          const f32x16 u = tile_pqT(tiles + tidx(I, p) * 1024, tiles + tidx(J, p) * 1024, lo, hi);
-          float* Aij = tiles + tidx(I, J) * 1024;
-#pragma unroll
-          for (int q = 0; q < 16; ++q) Aij[sw(acc_row(q, hi), lo)] -= u[q];
-        }
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---- back substitution x = L^-T y with the stored L_pp^-1 ----
-  // r_p = y_p - sum_{q>p} L_qp^T x_q   (one wave per q, partials in LDS)
-  // x_p = (L_pp^-1)^T r_p
-  for (int p = T - 1; p >= 0 && !(a.debug_skip & 16); --p) {
-    const int nq = T - 1 - p;  // < NW: one q per wave
-    if (wave < nq) {
-      const int q = p + 1 + wave;
-      const float* L = tiles + tidx(q, p) * 1024;
-      float pr = 0.0f;
-#pragma unroll 4
-      for (int m = 16 * hi; m < 16 * hi + 16; ++m) pr += L[sw(m, lo)] * xvec[32 * q + m];
-      pr += __shfl_xor(pr, 32);
-      if (hi == 0) part[wave * 32 + lo] = pr;
-    }
-    __syncthreads();
-    if (wave == 0) {
-      float r = bvec[32 * p + lo];
-      for (int w = 0; w < nq; ++w) r -= part[w * 32 + lo];
-      const float* Tpp = tiles + tidx(p, p) * 1024;
-      float x = 0.0f;
-#pragma unroll
-      for (int i = 0; i < 32; ++i) x += Tpp[sw(i, lo)] * rdlane(r, i);
-      if (hi == 0) xvec[32 * p + lo] = x;
-    }
-    __syncthreads();
-  }
+  // ---- blocked right-looking Cholesky with lookahead + back-solve ----
+  chol_solve_tiles<T, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
   if (tid < Dp) a.out[e * Dp + tid] = xvec[tid];
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
@@ -574,19 +478,20 @@ __global__ void __launch_bounds__(256) solve_small_kernel(SolveArgs a) {
   if (!ok) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
-template <int T>
+template <int T, bool PARTIAL>
 hipError_t launch_tiled(const SolveArgs& a, hipStream_t s) {
   using C = TiledCfg<T>;
   static bool attr = false;
   if (!attr) {
-    hipError_t err = hipFuncSetAttribute((const void*)solve_tiled_kernel<T>,
+    hipError_t err = hipFuncSetAttribute((const void*)solve_tiled_kernel<T, PARTIAL>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)C::BYTES);
     if (err != hipSuccess) return err;
     attr = true;
   }
-  hipLaunchKernelGGL(solve_tiled_kernel<T>, dim3((unsigned)a.n_rows), dim3(C::NTHR), C::BYTES, s,
-                     a);
+  const int64_t n = PARTIAL ? a.n_work : a.n_rows;
+  hipLaunchKernelGGL((solve_tiled_kernel<T, PARTIAL>), dim3((unsigned)n), dim3(C::NTHR), C::BYTES,
+                     s, a);
   return hipGetLastError();
 }
 
@@ -612,16 +517,36 @@ hipError_t launch_solve(int Dp, const SolveArgs& a, hipStream_t s) {
   switch (Dp) {
     case 8: return launch_small<8>(a, s);
     case 16: return launch_small<16>(a, s);
-    case 32: return launch_tiled<1>(a, s);
-    case 64: return launch_tiled<2>(a, s);
-    case 96: return launch_tiled<3>(a, s);
-    case 128: return launch_tiled<4>(a, s);
-    case 160: return launch_tiled<5>(a, s);
-    case 192: return launch_tiled<6>(a, s);
-    case 224: return launch_tiled<7>(a, s);
-    case 256: return launch_tiled<8>(a, s);
+    case 32: return launch_tiled<1, false>(a, s);
+    case 64: return launch_tiled<2, false>(a, s);
+    case 96: return launch_tiled<3, false>(a, s);
+    case 128: return launch_tiled<4, false>(a, s);
+    case 160: return launch_tiled<5, false>(a, s);
+    case 192: return launch_tiled<6, false>(a, s);
+    case 224: return launch_tiled<7, false>(a, s);
+    case 256: return launch_tiled<8, false>(a, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_split_syrk(int Dp, const SolveArgs& a, hipStream_t s) {
+  if (a.n_work <= 0) return hipSuccess;
+  switch (Dp) {
+    case 32: return launch_tiled<1, true>(a, s);
+    case 64: return launch_tiled<2, true>(a, s);
+    case 96: return launch_tiled<3, true>(a, s);
+    case 128: return launch_tiled<4, true>(a, s);
+    case 160: return launch_tiled<5, true>(a, s);
+    case 192: return launch_tiled<6, true>(a, s);
+    case 224: return launch_tiled<7, true>(a, s);
+    case 256: return launch_tiled<8, true>(a, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+size_t split_slab_floats(int Dp) {
+  const int T = Dp / 32;
+  return (size_t)T * (T + 1) / 2 * 1024 + Dp;
 }
 
 }  // namespace frecsys_hip

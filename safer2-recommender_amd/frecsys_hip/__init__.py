@@ -33,7 +33,7 @@ EXPORTS = (
     "frecsys_shard_range", "frecsys_load_csr", "frecsys_set_embeddings",
     "frecsys_get_embeddings", "frecsys_init_embeddings", "frecsys_snapshot",
     "frecsys_gramian", "frecsys_set_gramian", "frecsys_solve_side", "frecsys_user_loss",
-    "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset",
+    "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset", "frecsys_debug_basis",
 )
 
 
@@ -94,6 +94,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_synchronize": (ctypes.c_int, [P]),
         "frecsys_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, P]),
         "frecsys_timing_reset": (ctypes.c_int, [P]),
+        "frecsys_debug_basis": (ctypes.c_int, [P, I32, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -249,3 +250,12 @@ class Context:
 
     def timing_reset(self):
         self._check(self.lib.frecsys_timing_reset(self.h))
+
+    def debug_basis(self, side: int):
+        """(Q, diag, sub) with G[side] = Q T Q^T (diagnostic, Dp >= 64)."""
+        Dp = padded_dim(self.dim)
+        q = np.zeros((Dp, Dp), dtype=np.float32)
+        dg = np.zeros(Dp, dtype=np.float32)
+        sb = np.zeros(Dp, dtype=np.float32)
+        self._check(self.lib.frecsys_debug_basis(self.h, side, _ptr(q), _ptr(dg), _ptr(sb)))
+        return q, dg, sb

@@ -1,0 +1,176 @@
+"""History-space ("dual") solve path: the basis change G = Q T Q^T and the
+h x h push-through solve (dual.hip, spectral.hip) against the d-space solve
+and the CPU oracle.  The parity bar is the same as test_parity_gpu.py's
+(1e-4 relative per row); FRECSYS_DUAL=0 forces the d-space kernel for every
+entity, FRECSYS_DUAL_MAX_H moves the split between the two paths.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import rel_rows
+from test_parity_gpu import _ctx, _v_inputs, _weights
+
+pytestmark = pytest.mark.gpu
+
+fh = pytest.importorskip("frecsys_hip")
+
+TOL_ROW = 1e-4
+
+
+def _spread_embeddings(n, dim, seed):
+    """Rows with a wide, partly clustered spectrum (trained-model-like)."""
+    rng = np.random.default_rng(seed)
+    scales = np.geomspace(1.0, 0.03, dim)
+    scales[dim // 3: dim // 3 + 8] = 0.5  # a cluster of equal eigenvalues
+    return (rng.standard_normal((n, dim)) * scales).astype(np.float32)
+
+
+@pytest.mark.parametrize("dim", [64, 50, 96, 128, 200, 256])
+def test_basis_orthogonal_and_exact(quirk_data, dim):
+    nu, ni, up, uc, ip, ic = quirk_data
+    ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+    ctx.set_embeddings(fh.SIDE_USER, _spread_embeddings(nu, dim, 4))
+    G = ctx.gramian(fh.SIDE_USER).astype(np.float64)
+    Q, dg, sb = ctx.debug_basis(fh.SIDE_USER)
+    Dp = fh.padded_dim(dim)
+    Q = Q.astype(np.float64)
+    assert np.abs(Q.T @ Q - np.eye(Dp)).max() < 2e-6
+    T = np.diag(dg.astype(np.float64)) + np.diag(sb[:-1].astype(np.float64), -1) \
+        + np.diag(sb[:-1].astype(np.float64), 1)
+    Gp = np.zeros((Dp, Dp))
+    Gp[:dim, :dim] = G
+    err = np.abs(Q @ T @ Q.T - Gp).max() / np.abs(Gp).max()
+    assert err < 5e-6, err
+    # padded coordinates stay out of the basis: Q = diag(Q1, I)
+    if Dp > dim:
+        np.testing.assert_array_equal(Q[dim:, :dim], 0.0)
+        np.testing.assert_array_equal(Q[dim:, dim:], np.eye(Dp - dim))
+    assert sb[-1] == 0.0
+
+
+def _both_paths(monkeypatch, make, max_h=None):
+    outs = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("FRECSYS_DUAL", on)
+        if max_h is not None:
+            monkeypatch.setenv("FRECSYS_DUAL_MAX_H", str(max_h))
+        outs.append(make())
+    return outs
+
+
+@pytest.mark.parametrize("dim", [64, 96, 128, 256])
+@pytest.mark.parametrize("max_h", [256, 64])
+def test_ials_dual_vs_dspace_vs_oracle(monkeypatch, quirk_data, dim, max_h):
+    nu, ni, up, uc, ip, ic = quirk_data
+    reg, w = 0.003, 0.1
+    V0 = _spread_embeddings(ni, dim, 8)
+
+    def run():
+        ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+        ctx.set_embeddings(fh.SIDE_ITEM, V0)
+        ctx.gramian(fh.SIDE_ITEM)
+        ctx.timing_reset()
+        ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, reg, w)
+        hs = ctx.timing("solve_user.hspace")[1]
+        return ctx.get_embeddings(fh.SIDE_USER), U, hs
+
+    (Ud, U, hs0), (Uh, _, hs1) = _both_paths(monkeypatch, run, max_h)
+    assert hs0 == 0 and hs1 == 1  # the split really happened
+    Uo, rc = O.step(up, uc, V0, O.gramian(V0), 0, reg, w, out=U.copy())
+    assert rc == 0
+    assert rel_rows(Ud, Uo).max() < TOL_ROW
+    assert rel_rows(Uh, Uo).max() < TOL_ROW
+    np.testing.assert_array_equal(Uh[5], U[5])  # idle user untouched
+    h = np.diff(up)
+    long = h > max_h
+    np.testing.assert_array_equal(Uh[long], Ud[long])  # same kernel for the long ones
+
+
+@pytest.mark.parametrize("dim", [64, 128, 256])
+def test_weighted_u_dual(monkeypatch, quirk_data, dim):
+    nu, ni, up, uc, ip, ic = quirk_data
+    om = _weights(nu)
+    om[::7] = 0.0  # zero dual weights: the row must come out exactly 0
+    reg, w = 0.004, 0.004
+    V0 = _spread_embeddings(ni, dim, 9)
+
+    def run():
+        ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+        ctx.set_embeddings(fh.SIDE_ITEM, V0)
+        ctx.gramian(fh.SIDE_ITEM)
+        ctx.solve_side(fh.SIDE_USER, fh.KIND_WEIGHTED_U, reg, w, entity_weight=om)
+        return ctx.get_embeddings(fh.SIDE_USER), U
+
+    (Ud, U), (Uh, _) = _both_paths(monkeypatch, run)
+    Uo, rc = O.step(up, uc, V0, O.gramian(V0), 1, reg, w, entity_weight=om, out=U.copy())
+    assert rc == 0
+    assert rel_rows(Uh, Uo).max() < TOL_ROW
+    assert rel_rows(Ud, Uo).max() < TOL_ROW
+    zero = (om == 0) & (np.diff(up) > 0)
+    assert np.abs(Uh[zero]).max() == 0.0
+
+
+@pytest.mark.parametrize("dim", [64, 160, 256])
+@pytest.mark.parametrize("quirk", [True, False])
+def test_weighted_v_dual(monkeypatch, quirk_data, dim, quirk):
+    nu, ni, up, uc, ip, ic = quirk_data
+    om = _weights(nu)
+    om[::5] = 0.0  # users with zero weight contribute nothing (CVaR-style)
+    nu_w, item_reg = _v_inputs(nu, ni, up, ip, ic, om)
+    reg, w, alpha = 0.004, 0.004, 0.3
+    U0 = _spread_embeddings(nu, dim, 10)
+
+    def run():
+        ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic, quirks=quirk)
+        ctx.set_embeddings(fh.SIDE_USER, U0)
+        ctx.gramian(fh.SIDE_USER, weights=om)
+        ctx.solve_side(fh.SIDE_ITEM, fh.KIND_WEIGHTED_V, reg, w, alpha=alpha,
+                       entity_reg=item_reg, other_weight=nu_w)
+        return ctx.get_embeddings(fh.SIDE_ITEM), V
+
+    (Vd, V), (Vh, _) = _both_paths(monkeypatch, run)
+    Vo, rc = O.step(ip, ic, U0, O.gramian(U0, om), 2, reg, w, alpha=alpha, quirk=int(quirk),
+                    entity_reg=item_reg, other_weight=nu_w, out=V.copy())
+    assert rc == 0
+    assert rel_rows(Vh, Vo).max() < TOL_ROW
+    assert rel_rows(Vd, Vo).max() < TOL_ROW
+
+
+def test_tail_quirk_in_history_space(monkeypatch, quirk_data):
+    """Quirk rows (A only, not b) must matter in the history-space form too."""
+    nu, ni, up, uc, ip, ic = quirk_data
+    monkeypatch.setenv("FRECSYS_DUAL", "1")
+    dim = 64
+    om = _weights(nu)
+    nu_w, item_reg = _v_inputs(nu, ni, up, ip, ic, om)
+    outs = []
+    for q in (True, False):
+        ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic, quirks=q)
+        ctx.gramian(fh.SIDE_USER, weights=om)
+        ctx.solve_side(fh.SIDE_ITEM, fh.KIND_WEIGHTED_V, 0.004, 0.004, alpha=0.3,
+                       entity_reg=item_reg, other_weight=nu_w)
+        outs.append(ctx.get_embeddings(fh.SIDE_ITEM))
+    h = np.diff(ip)
+    affected = (h > 128) & (h % 128 != 0) & (h + 128 - h % 128 <= 256)
+    assert affected.sum() >= 2
+    diff = np.abs(outs[0] - outs[1]).max(axis=1)
+    assert (diff[affected] > 0).all()
+    np.testing.assert_array_equal(outs[0][h <= 128], outs[1][h <= 128])
+
+
+def test_eval_side_dual(monkeypatch, ml1m):
+    monkeypatch.setenv("FRECSYS_DUAL", "1")
+    tr, vt, ve = ml1m
+    nu, ni = tr.max_user + 1, tr.max_item + 1
+    up, uc = tr.by_user()
+    ip, ic = tr.by_item()
+    ctx, U, V = _ctx(128, nu, ni, up, uc, ip, ic)
+    V0 = _spread_embeddings(ni, 128, 11)
+    ctx.set_embeddings(fh.SIDE_ITEM, V0)
+    ids, ep, ec = vt.compact_users()
+    ctx.load_csr(fh.SIDE_EVAL, ep, ec)
+    ctx.gramian(fh.SIDE_ITEM)
+    ctx.solve_side(fh.SIDE_EVAL, fh.KIND_IALS, 0.003, 0.1)
+    Uo, rc = O.step(ep, ec, V0, O.gramian(V0), 0, 0.003, 0.1)
+    assert rel_rows(ctx.get_embeddings(fh.SIDE_EVAL), Uo).max() < TOL_ROW
