@@ -780,7 +780,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
   shard(c, side, &lo, &hi);
   rc = build_order(c, side);
   if (rc) return rc;
-  SolveArgs a;
+  SolveArgs a{};
   a.kind = kind;
   a.order = c->d_order[side];
   a.counter = c->d_counter;
@@ -880,7 +880,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       rc = ensure(c, &c->out_rot[side], &c->cap_out_rot[side],
                   (size_t)std::max<int64_t>(c->n[side], 1) * c->Dp);
       if (rc) return rc;
-      DualArgs d;
+      DualArgs d{};
       d.kind = kind;
       d.quirk = c->quirks;
       d.Dp = c->Dp;
@@ -899,6 +899,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       d.entity_reg = a.entity_reg;
       d.other_weight = a.other_weight;
       d.fail = a.fail;
+      d.debug_skip = a.debug_skip;
       const int64_t n_hs = n_nonempty - n_dspace;
       rc = ensure(c, &c->dual_table, &c->cap_dual_table, (size_t)n_hs * 3 * c->Dp);
       if (rc) return rc;

@@ -27,22 +27,32 @@ __device__ __forceinline__ float rdlane(float v, int l) {
 // lookahead) overflow the SGPRs and the spills push the kernels to 256
 // VGPRs (occupancy 1-2); as a call it costs nothing measurable.
 // ---------------------------------------------------------------------
-__device__ __noinline__ bool diag_factor_inv(float* tile, int lane) {
+typedef __attribute__((address_space(3))) float lds_float;
+
+__device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
   const int r = lane & 31;
   const bool fl = lane < 32;
   float a[32];
 #pragma unroll
-  for (int c = 0; c < 32; ++c) a[c] = fl ? tile[sw(r, c)] : (c == r ? 1.0f : 0.0f);
+  for (int c = 0; c < 32; ++c) {
+    const float t = tile[sw(r, c)];  // both halves read (no divergent loads)
+    a[c] = fl ? t : (c == r ? 1.0f : 0.0f);
+  }
   bool ok = true;
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
     float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
 #pragma unroll
     for (int m = 0; m < k; m += 4) {
-      p0 += a[m] * rdlane(a[m], k);
-      if (m + 1 < k) p1 += a[m + 1] * rdlane(a[m + 1], k);
-      if (m + 2 < k) p2 += a[m + 2] * rdlane(a[m + 2], k);
-      if (m + 3 < k) p3 += a[m + 3] * rdlane(a[m + 3], k);
+      // broadcasts first, then the FMAs: no SGPR-hazard nop per pair
+      const float b0 = rdlane(a[m], k);
+      const float b1 = m + 1 < k ? rdlane(a[m + 1], k) : 0.0f;
+      const float b2 = m + 2 < k ? rdlane(a[m + 2], k) : 0.0f;
+      const float b3 = m + 3 < k ? rdlane(a[m + 3], k) : 0.0f;
+      p0 += a[m] * b0;
+      if (m + 1 < k) p1 += a[m + 1] * b1;
+      if (m + 2 < k) p2 += a[m + 2] * b2;
+      if (m + 3 < k) p3 += a[m + 3] * b3;
     }
     const float t = a[k] - ((p0 + p1) + (p2 + p3));
     const float piv = rdlane(t, k);
@@ -51,12 +61,16 @@ __device__ __noinline__ bool diag_factor_inv(float* tile, int lane) {
     const float rd = 1.0f / d;
     a[k] = (lane == k) ? d : t * rd;
   }
-  if (!fl) {  // column j of L^-1 -> tile element (k, j), k >= j
-    const int j = r;
+  // lanes 32..63: column j of L^-1 -> tile element (k, j), k >= j
+  const int j = r;
 #pragma unroll
-    for (int k = 0; k < 32; ++k) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
-  }
+  for (int k = 0; k < 32; ++k)
+    if (!fl) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
   return ok;
+}
+
+__device__ __forceinline__ bool diag_factor_inv(float* tile, int lane) {
+  return diag_factor_inv_lds((lds_float*)tile, lane);
 }
 
 // One 32x32 MFMA product u = P Q^T of two LDS tiles (P, Q swizzled).

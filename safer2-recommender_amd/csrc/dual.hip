@@ -228,8 +228,8 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
   {  // l_k and D^-1/2 from the entity's table row
     const float* trow = a.table + (int64_t)blockIdx.x * 3 * Dp;
     for (int k = tid; k < Dp; k += NTHR) {
-      lsub[k] = trow[k];
-      dsq[k] = trow[Dp + k];
+      lsub[k] = (a.debug_skip & 256) ? 0.5f : trow[k];
+      dsq[k] = (a.debug_skip & 256) ? 0.5f : trow[Dp + k];
     }
   }
   __syncthreads();
@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       if ((HP * 8) % NTHR == 0 || s < HP * 8) {
         const int r = s >> 3, c4 = s & 7;
         const int id = ids[r];
-        if (id >= 0)
+        if (id >= 0 && !(a.debug_skip & 32))
           regs[q] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)id * Dp + 32 * c + 4 * c4);
       }
     }
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
   for (int c = 0; c < NC; ++c) {
     const bool more = c + 1 < NC;
     if (more) load_slab(c + 1);
-    if (tid < HP) {
+    if (tid < HP && !(a.debug_skip & 128)) {
       const float* yrow = stage + tid * SROW;
       float y[32];
 #pragma unroll
@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       const float* zr = zs + (2 * s + hi) * HP;
 #pragma unroll
       for (int m = 0; m < MT; ++m)
-        if (valid[m]) acc[m] = mfma32(zr[aoff[m]], zr[boff[m]], acc[m]);
+        if (valid[m] && !(a.debug_skip & 1)) acc[m] = mfma32(zr[aoff[m]], zr[boff[m]], acc[m]);
     }
     if (more) store_slab();
     __syncthreads();
@@ -328,7 +328,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
     }
   }
   __syncthreads();
-  chol_solve_tiles<TH, NW>(tiles, bvec, xvec, part, flag, tid, 0);
+  chol_solve_tiles<TH, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
 
   // ---- v = Y^T (c.*z): the rows again, float4 per lane, 8 rows in flight ----
   {
@@ -336,7 +336,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
     const int c4 = tid % D4, g = tid / D4;
     float* red = tiles;  // the S tiles are dead after the solve
     float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (g < R) {
+    if (g < R && !(a.debug_skip & 64)) {
       for (int j0 = g; j0 < ntot; j0 += 8 * R) {
         float4 rv[8];
         float wv[8];
@@ -368,6 +368,251 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
     }
   }
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
+}
+
+
+// ---------------------------------------------------------------------
+// Short histories (h_eff <= 64): one wave per entity, four independent
+// entities per workgroup, no workgroup barrier anywhere.  Lane j owns
+// history row j: it loads the row's 32-column slab straight into registers
+// (one slab ahead), runs the bidiagonal recurrence with l_k and D^-1/2 as
+// wave-uniform scalars from the entity's table row, and writes the scaled
+// values k-major to its wave's LDS slab; the same wave then accumulates
+// the S tiles with MFMA, factors S (chol_solve_wave) and forms Y^T (c.*z)
+// with coalesced whole-row loads.
+// ---------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// chol_solve_tiles for one wave (T <= 2): x = S^-1 b, S's lower tiles in
+// LDS (swizzled), diagonal tiles become L_pp^-1.
+template <int T>
+__device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float* xvec,
+                                                int* flag, int lane, int debug_skip) {
+  const int lo = lane & 31, hi = lane >> 5;
+  float y[T];
+#pragma unroll
+  for (int p = 0; p < T; ++p) {
+    float* Tpp = tiles + tidx(p, p) * 1024;
+    if (!(debug_skip & 2) && !diag_factor_inv(Tpp, lane) && lane == 0) flag[0] = 1;
+    wave_sync();
+    // y_p = L_pp^-1 b_p  (lane lo, both halves compute, half 0 keeps it)
+    float yp = 0.0f;
+#pragma unroll 8
+    for (int k = 0; k < 32; ++k) yp += Tpp[sw(lo, k)] * bvec[32 * p + k];
+    y[p] = yp;
+    if (hi == 0) xvec[32 * p + lo] = yp;  // y staged for the panel update
+    if (p + 1 < T) {
+      float* A10 = tiles + tidx(p + 1, p) * 1024;
+      const f32x16 u = tile_pqT(A10, Tpp, lo, hi);  // L_10 = A_10 L_00^-T
+      wave_sync();
+#pragma unroll
+      for (int q = 0; q < 16; ++q) A10[sw(acc_row(q, hi), lo)] = u[q];
+      wave_sync();
+      // b_1 -= L_10 y_0 ; A_11 -= L_10 L_10^T
+      float t = 0.0f;
+#pragma unroll 8
+      for (int k = 0; k < 32; ++k) t += A10[sw(lo, k)] * xvec[32 * p + k];
+      const f32x16 w = tile_pqT(A10, A10, lo, hi);
+      float* A11 = tiles + tidx(p + 1, p + 1) * 1024;
+      wave_sync();
+      if (hi == 0) bvec[32 * (p + 1) + lo] -= t;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) A11[sw(acc_row(q, hi), lo)] -= w[q];
+      wave_sync();
+    }
+  }
+  // back substitution
+  float x1 = 0.0f;
+  if (T == 2) {
+    const float* T11 = tiles + tidx(1, 1) * 1024;
+    float x = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) x += T11[sw(i, lo)] * rdlane(y[1], i);
+    x1 = x;
+    if (hi == 0) xvec[32 + lo] = x;
+    wave_sync();
+  }
+  float r = y[0];
+  if (T == 2) {  // r_0 = y_0 - L_10^T x_1
+    const float* L10 = tiles + tidx(1, 0) * 1024;
+    float t = 0.0f;
+#pragma unroll 8
+    for (int m = 0; m < 32; ++m) t += L10[sw(m, lo)] * xvec[32 + m];
+    r -= t;
+  }
+  const float* T00 = tiles;
+  float x = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) x += T00[sw(i, lo)] * rdlane(r, i);
+  wave_sync();
+  if (hi == 0) xvec[lo] = x;
+  (void)x1;
+  wave_sync();
+}
+
+template <int TH>
+struct WaveCfg {
+  static constexpr int HP = 32 * TH;
+  static constexpr int NT = TH * (TH + 1) / 2;
+  static constexpr int ZS = 32 * HP;
+  static constexpr int REG = NT * 1024 > ZS ? NT * 1024 : ZS;
+  static constexpr int OFF_ID = REG, OFF_C = OFF_ID + HP, OFF_B = OFF_C + HP, OFF_X = OFF_B + HP;
+  static constexpr int OFF_FLAG = OFF_X + HP;
+  static constexpr int PW = OFF_FLAG + 4;  // floats per wave
+  static constexpr size_t BYTES = (size_t)4 * PW * 4;
+  static_assert(TH <= 2, "one history row per lane");
+};
+
+template <int TH>
+__global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
+  using C = WaveCfg<TH>;
+  constexpr int HP = C::HP, NT = C::NT;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lo = lane & 31, hi = lane >> 5;
+  const int64_t pos = (int64_t)blockIdx.x * 4 + wave;
+  if (pos >= a.n_rows) return;  // whole wave; no workgroup barriers below
+  float* base = smem + wave * C::PW;
+  float* zs = base;
+  float* tiles = base;
+  int* ids = reinterpret_cast<int*>(base + C::OFF_ID);
+  float* cvec = base + C::OFF_C;
+  float* bvec = base + C::OFF_B;
+  float* xvec = base + C::OFF_X;
+  int* flag = reinterpret_cast<int*>(base + C::OFF_FLAG);
+
+  const int kind = a.kind;
+  const bool vk = is_v_kind(kind), uk = is_u_kind(kind);
+  const int Dp = a.Dp, NC = Dp >> 5;
+  const QueueRec rec = a.order[pos];
+  const int64_t e = rec.entity, h = rec.h, p0 = rec.p0;
+  int64_t extra = 0;
+  if (vk && a.quirk && h > 128 && (h % 128) != 0) extra = 128 - (h % 128);
+  const int ntot = (int)(h + extra);
+  float mu, lam, omega;
+  dual_scalars(a, e, h, mu, lam, omega);
+  (void)mu;
+  (void)lam;
+  const float hf = (float)h;
+
+  // my history row
+  const int j = lane;
+  int id = -1;
+  float cj = 0.0f;
+  if (j < ntot) {
+    id = a.col[p0 + virt_pos_d(j, h)];
+    cj = vk ? sqrtf(a.other_weight[id]) : (uk ? sqrtf(omega / hf) : 1.0f);
+  }
+  if (j < HP) {
+    ids[j] = id;
+    cvec[j] = cj;
+    bvec[j] = j < h ? cj : 0.0f;
+  }
+  if (lane == 0) flag[0] = 0;
+  const float* trow = a.table + pos * 3 * Dp;  // wave-uniform
+  const float* xrow = a.Xrot + (int64_t)(id < 0 ? 0 : id) * Dp;
+
+  float4 yr[8], yn[8];
+  auto load = [&](int c, float4* dst) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      dst[q] = (id >= 0 && !(a.debug_skip & 32))
+                   ? *reinterpret_cast<const float4*>(xrow + 32 * c + 4 * q)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  load(0, yr);
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
+  float carry = 0.0f;
+  for (int c = 0; c < NC; ++c) {
+    if (c + 1 < NC) load(c + 1, yn);
+    if (j < HP && !(a.debug_skip & 128)) {
+      float z = carry;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float yv[4] = {yr[q].x, yr[q].y, yr[q].z, yr[q].w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = 4 * q + u, k = 32 * c + kk;
+          z = yv[u] - trow[k] * z;
+          zs[kk * HP + j] = (cj * z) * trow[Dp + k];
+        }
+      }
+      carry = z;
+    }
+    wave_sync();
+#pragma unroll 4
+    for (int s2 = 0; s2 < 16; ++s2) {
+      const float* zr = zs + (2 * s2 + hi) * HP;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= t) ++I;
+        const int J = t - I * (I + 1) / 2;
+        if (!(a.debug_skip & 1)) acc[t] = mfma32(zr[32 * I + lo], zr[32 * J + lo], acc[t]);
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) yr[q] = yn[q];
+  }
+  // S = I + acc
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    float* tile = tiles + t * 1024;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = acc_row(q, hi);
+      tile[sw(i, lo)] = acc[t][q] + ((32 * I + i) == (32 * J + lo) ? 1.0f : 0.0f);
+    }
+  }
+  wave_sync();
+  chol_solve_wave<TH>(tiles, bvec, xvec, flag, lane, a.debug_skip);
+
+  // v = Y^T (c.*z): lane owns columns 4*lane .. 4*lane+3
+  float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (4 * lane < Dp && !(a.debug_skip & 64)) {
+    for (int j0 = 0; j0 < ntot; j0 += 8) {
+      float4 rv[8];
+      float wv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int jj = j0 + u;
+        wv[u] = 0.0f;
+        rv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (jj < ntot) {
+          wv[u] = cvec[jj] * xvec[jj];
+          rv[u] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)ids[jj] * Dp + 4 * lane);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v4.x += wv[u] * rv[u].x;
+        v4.y += wv[u] * rv[u].y;
+        v4.z += wv[u] * rv[u].z;
+        v4.w += wv[u] * rv[u].w;
+      }
+    }
+  }
+  if (4 * lane < Dp) *reinterpret_cast<float4*>(a.out_rot + e * Dp + 4 * lane) = v4;
+  if (lane == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
+}
+
+template <int TH>
+hipError_t launch_wave_t(const DualArgs& a, hipStream_t s) {
+  using C = WaveCfg<TH>;
+  const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
+  hipLaunchKernelGGL(dual_wave_kernel<TH>, dim3(nb), dim3(256), C::BYTES, s, a);
+  return hipGetLastError();
 }
 
 template <int TH>
@@ -407,8 +652,8 @@ hipError_t launch_dual(int tiles, const DualArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
   if (a.Dp < 64 || a.Dp > kMaxDp || (a.Dp & 31)) return hipErrorInvalidValue;
   switch (tiles) {
-    case 1: return launch_dual_t<1>(a, s);
-    case 2: return launch_dual_t<2>(a, s);
+    case 1: return a.debug_skip & 512 ? launch_dual_t<1>(a, s) : launch_wave_t<1>(a, s);
+    case 2: return a.debug_skip & 512 ? launch_dual_t<2>(a, s) : launch_wave_t<2>(a, s);
     case 3: return launch_dual_t<3>(a, s);
     case 4: return launch_dual_t<4>(a, s);
     case 5: return launch_dual_t<5>(a, s);

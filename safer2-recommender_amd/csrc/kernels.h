@@ -105,6 +105,7 @@ struct DualArgs {
   const float* entity_reg;
   const float* other_weight;
   unsigned long long* fail;
+  int debug_skip;  // ablation only: 1 SYRK, 2/4/8/16 Cholesky parts, 64 Y^T z, 128 recurrence
 };
 
 // Largest history-space tile count built (h_eff <= 32 * kDualMaxTiles).

@@ -7,9 +7,9 @@
 // ials.h:101-131); this is the MI355X re-design that lets the short-history
 // entities solve an h x h system instead.
 //
-//  tridiag_kernel  one workgroup, 16 waves: Householder reduction of the
-//                  lower-packed matrix held in LDS (Dp(Dp+1)/2 floats, 129 KB
-//                  at Dp = 256), LAPACK sytd2 conventions (v(k+1) = 1).
+//  tridiag_kernel  one workgroup, 16 waves: Householder reduction with the
+//                  matrix in registers (an 8 x 8 block per thread), LAPACK
+//                  sytd2 conventions (v(k+1) = 1).
 //  form_q_kernel   Q = H_0 ... H_{n-3}, one wave per column of Q.
 //  rot_gemm_kernel 64 rows x Dp columns per workgroup, v_mfma_f32_32x32x2_f32,
 //                  the row block in LDS and Q streamed through LDS by 32-row
@@ -29,90 +29,168 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// packed lower index, i >= j
-__device__ __forceinline__ int pk(int i, int j) { return i * (i + 1) / 2 + j; }
+// Sum over a full wave with DPP row ops (no LDS round trips); every lane
+// gets the total.
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  auto dpp = [](float x, int ctrl, int row_mask) -> float {
+    switch (ctrl) {  // the control word must be a compile-time constant
+      case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
+      case 0x4E: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));
+      case 0x141: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));
+      case 0x140: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x140, 0xF, 0xF, false));
+      case 0x142: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x142, 0xA, 0xF, false));
+      default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x143, 0xC, 0xF, false));
+    }
+    (void)row_mask;
+  };
+  v += dpp(v, 0xB1, 0xF);   // quad_perm [1,0,3,2]
+  v += dpp(v, 0x4E, 0xF);   // quad_perm [2,3,0,1]
+  v += dpp(v, 0x141, 0xF);  // row_half_mirror
+  v += dpp(v, 0x140, 0xF);  // row_mirror: 16-lane row sums
+  v += dpp(v, 0x142, 0xA);  // row_bcast15 into rows 1, 3
+  v += dpp(v, 0x143, 0xC);  // row_bcast31 into rows 2, 3: lane 63 = total
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
 
+// Householder tridiagonalisation, register-resident: the 1024 threads hold
+// the FULL symmetric matrix (zero-padded to 256) as 8 x 8 blocks; thread
+// t owns block row bi = t & 31 of block column bj = t >> 5, so the owners
+// of one block column are 32 lanes of one wave.  Step k (LAPACK sytd2,
+// lower): the wave owning column k forms the reflector v (v_{k+1} = 1),
+// tau, beta right after its own update of step k-1 and publishes v;
+// p = tau A v (8x8 block products, partial row sums reduced through LDS,
+// v^T A v reduced alongside for K); w = p - K v, K = (tau/2) v.p;
+// A -= v w^T + w v^T on the whole matrix -- v is zero on rows <= k, so this
+// is exactly H A H and the trailing block sees the textbook arithmetic.
+// Three barriers per step.
 __global__ void __launch_bounds__(1024)
     tridiag_kernel(const float* __restrict__ G, int n, float* tdiag, float* toff, float* Vh,
                    float* tau_out) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int np = n * (n + 1) / 2;
-  float* P = sm;
-  float* v = P + np;
-  float* p = v + n;
-  float* part = p + n;      // [4][256]
-  float* sc = part + 1024;  // [0..1] tau slots, [4..7] dot partials
+  __shared__ float vs[2][256];
+  __shared__ float ps[256];
+  __shared__ float part[32 * 257];
+  __shared__ float red[2][16];
+  __shared__ float tsh[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = wave; i < n; i += 16)
-    for (int j = lane; j <= i; j += 64) P[pk(i, j)] = G[(int64_t)i * n + j];
+  const int bi = tid & 31, bj = tid >> 5;
+  const int r0 = 8 * bi, c0 = 8 * bj;
+  float A[8][8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      A[r][c] = (r0 + r < n && c0 + c < n) ? G[(int64_t)(r0 + r) * n + c0 + c] : 0.0f;
+
+  // reflector for column k, by the wave that owns it (lanes of block col k>>3)
+  auto reflector = [&](int k) {
+    const int kb = k >> 3, cc = k & 7;
+    if (wave != (kb >> 1)) return;
+    const bool mine = bj == kb;  // my half of the wave holds column k
+    float x[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float t = 0.0f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) t = (c == cc) ? A[r][c] : t;
+      x[r] = mine ? t : 0.0f;
+    }
+    float s = 0.0f, x0 = 0.0f, dkk = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int i = r0 + r;
+      if (i >= k + 2) s += x[r] * x[r];
+      if (i == k + 1) x0 = x[r];
+      if (i == k) dkk = x[r];
+    }
+    s = wave_sum_dpp(s);
+    x0 = wave_sum_dpp(x0);
+    dkk = wave_sum_dpp(dkk);
+    float tau = 0.0f, beta = x0, scal = 0.0f;
+    if (s > 0.0f) {
+      const float nrm = sqrtf(x0 * x0 + s);
+      beta = x0 >= 0.0f ? -nrm : nrm;
+      tau = (beta - x0) / beta;
+      scal = 1.0f / (x0 - beta);
+    }
+    float* v = vs[k & 1];
+    if (mine) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int i = r0 + r;
+        float vi = 0.0f;
+        if (i == k + 1) vi = 1.0f;
+        else if (i > k + 1) vi = x[r] * scal;
+        v[i] = tau != 0.0f ? vi : 0.0f;
+        if (i > k && i < n) Vh[(int64_t)k * n + i] = vi;
+      }
+    }
+    if (lane == 0) {
+      tsh[k & 1] = tau;
+      tdiag[k] = dkk;
+      toff[k] = beta;
+      tau_out[k] = tau;
+    }
+  };
+
+  if (n > 2) reflector(0);
   __syncthreads();
   for (int k = 0; k < n - 2; ++k) {
-    const int m = n - k - 1;
-    if (wave == 0) {
-      // reflector for column k below the diagonal (LAPACK slarfg)
-      const float x0 = P[pk(k + 1, k)];
-      float s = 0.0f;
-      for (int i = k + 2 + lane; i < n; i += 64) {
-        const float x = P[pk(i, k)];
-        s += x * x;
+    const float tau = tsh[k & 1];
+    const float* v = vs[k & 1];
+    if (tau != 0.0f) {
+      // p partials over my 8 columns; v^T (A v) partial for K
+      float vc[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) vc[c] = v[c0 + c];
+      float vav = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc += A[r][c] * vc[c];
+        part[bj * 257 + r0 + r] = acc;
+        vav += v[r0 + r] * acc;
       }
-      s = wave_sum(s);
-      float tau = 0.0f, beta = x0, scal = 0.0f;
-      if (s > 0.0f) {
-        const float nrm = sqrtf(x0 * x0 + s);
-        beta = x0 >= 0.0f ? -nrm : nrm;
-        tau = (beta - x0) / beta;
-        scal = 1.0f / (x0 - beta);
+      vav = wave_sum_dpp(vav);
+      if (lane == 0) red[k & 1][wave] = vav;
+      __syncthreads();
+      if (tid < 256) {
+        float acc = 0.0f;
+#pragma unroll 8
+        for (int j = 0; j < 32; ++j) acc += part[j * 257 + tid];
+        ps[tid] = tau * acc;
       }
-      for (int i = k + 1 + lane; i < n; i += 64) {
-        const float vi = (i == k + 1) ? 1.0f : P[pk(i, k)] * scal;
-        v[i] = vi;
-        Vh[(int64_t)k * n + i] = vi;
-      }
-      if (lane == 0) {
-        sc[k & 1] = tau;
-        tdiag[k] = P[pk(k, k)];
-        toff[k] = beta;
-        tau_out[k] = tau;
-      }
-    }
-    __syncthreads();
-    const float tau = sc[k & 1];
-    if (tau == 0.0f) continue;  // column already reduced: A22 unchanged
-    // p = tau * A22 v, four threads per row
-    const int ro = tid >> 2, t = tid & 3;
-    const int i = k + 1 + ro;
-    float acc = 0.0f;
-    if (i < n) {
-      for (int j = k + 1 + t; j < n; j += 4) acc += P[j <= i ? pk(i, j) : pk(j, i)] * v[j];
-    }
-    part[t * 256 + ro] = acc;
-    __syncthreads();
-    float dp = 0.0f;
-    if (tid < m) {
-      const int ii = k + 1 + tid;
-      const float pi = tau * ((part[tid] + part[256 + tid]) + (part[512 + tid] + part[768 + tid]));
-      p[ii] = pi;
-      dp = pi * v[ii];
-    }
-    dp = wave_sum(dp);
-    if (lane == 0 && wave < 4) sc[4 + wave] = dp;
-    __syncthreads();
-    const float K = 0.5f * tau * ((sc[4] + sc[5]) + (sc[6] + sc[7]));
-    // A22 -= v w^T + w v^T,  w = p - K v
-    if (i < n) {
-      const float vi = v[i], wi = p[i] - K * vi;
-      for (int j = k + 1 + t; j <= i; j += 4) {
-        const float vj = v[j], wj = p[j] - K * vj;
-        P[pk(i, j)] -= vi * wj + wi * vj;
+      float vAv = 0.0f;
+#pragma unroll
+      for (int w = 0; w < 16; ++w) vAv += red[k & 1][w];
+      const float K = 0.5f * tau * tau * vAv;
+      __syncthreads();
+      // A -= v w^T + w v^T
+      float wc[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) wc[c] = ps[c0 + c] - K * vc[c];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float vr = v[r0 + r];
+        const float wr = ps[r0 + r] - K * vr;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) A[r][c] -= vr * wc[c] + wr * vc[c];
       }
     }
+    if (k + 1 < n - 2) reflector(k + 1);
     __syncthreads();
   }
+  // the last 2 x 2 block
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int i = r0 + r, j = c0 + c;
+      if (i == n - 2 && j == n - 2) tdiag[n - 2] = A[r][c];
+      if (i == n - 1 && j == n - 1) tdiag[n - 1] = A[r][c];
+      if (i == n - 1 && j == n - 2) toff[n - 2] = A[r][c];
+    }
   if (tid == 0) {
-    tdiag[n - 2] = P[pk(n - 2, n - 2)];
-    tdiag[n - 1] = P[pk(n - 1, n - 1)];
-    toff[n - 2] = P[pk(n - 1, n - 2)];
     toff[n - 1] = 0.0f;
     tau_out[n - 2] = 0.0f;
     tau_out[n - 1] = 0.0f;
@@ -249,15 +327,7 @@ hipError_t launch_rot(const float* X, const QueueRec* rows, int64_t r0, int64_t 
 hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
                           float* tau, hipStream_t s) {
   if (Dp < 4 || Dp > 256) return hipErrorInvalidValue;
-  const size_t bytes = sizeof(float) * ((size_t)Dp * (Dp + 1) / 2 + 2 * Dp + 1024 + 8);
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)tridiag_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(1024), bytes, s, G, Dp, tdiag, toff, Vh, tau);
+  hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(1024), 0, s, G, Dp, tdiag, toff, Vh, tau);
   return hipGetLastError();
 }
 

@@ -24,10 +24,13 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
                 ctx.solve_side(side, 0, 0.003, 0.1)
             except fh.FrecsysError:
                 pass
-    print(json.dumps({"mask": int(os.environ.get("FRECSYS_DEBUG_SKIP", "0")),
-                      "user_ms": ctx.timing("solve_user")[0] / 2, "item_ms": ctx.timing("solve_item")[0] / 2}))
+    out = {"mask": int(os.environ.get("FRECSYS_DEBUG_SKIP", "0"))}
+    for side in ("solve_user", "solve_item"):
+        for part in ("", ".dspace", ".basis", ".hspace", ".rotate"):
+            out[side + part] = round(ctx.timing(side + part)[0] / 2, 3)
+    print(json.dumps(out))
     sys.exit(0)
 for mask in [int(m) for m in (sys.argv[1:] or ["0", "1", "2", "4", "8", "16", "30", "31"])]:
-    env = dict(os.environ, FRECSYS_DEBUG_SKIP=str(mask))
+    env = dict(os.environ, FRECSYS_DEBUG_SKIP=str(mask), FRECSYS_DUAL_SERIAL="1")
     out = subprocess.run([sys.executable, __file__, "child"], env=env, capture_output=True, text=True, timeout=300)
     print(out.stdout.strip() or out.stderr[-500:], flush=True)
