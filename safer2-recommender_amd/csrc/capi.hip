@@ -64,6 +64,8 @@ struct frecsys_ctx {
   size_t cap_partials = 0;
   float* d_loss = nullptr;
   size_t cap_loss = 0;
+  float* d_quad = nullptr;
+  size_t cap_quad = 0;
   unsigned long long* d_fail = nullptr;
   unsigned int* d_counter = nullptr;
   // per side: the rank's entities in decreasing-history order (LPT queue)
@@ -515,7 +517,7 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
     if (c->gram[s]) (void)hipFree(c->gram[s]);
   }
   for (float* p : {c->d_entity_weight, c->d_entity_reg, c->d_other_weight, c->d_gram_w,
-                   c->d_partials, c->d_loss})
+                   c->d_partials, c->d_loss, c->d_quad})
     if (p) (void)hipFree(p);
   if (c->d_fail) (void)hipFree(c->d_fail);
   if (c->d_counter) (void)hipFree(c->d_counter);
@@ -974,7 +976,10 @@ int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, fl
     HIP_TRY(c, hipMemsetAsync(c->d_loss, 0, sizeof(float) * std::max<size_t>(rows, 1), c->stream));
   int64_t lo, hi;
   shard(c, side, &lo, &hi);
-  LossArgs a;
+  rc = ensure(c, &c->d_quad, &c->cap_quad, std::max<size_t>(rows, 1));
+  if (rc) return rc;
+  LossArgs a{};
+  a.quad = c->d_quad;
   a.row_ptr = c->rp[side];
   a.col = c->col[side];
   a.row_lo = lo;

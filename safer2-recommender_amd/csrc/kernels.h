@@ -73,6 +73,7 @@ struct LossArgs {
   float beta;
   int half;
   float* out;            // [rows of side]
+  float* quad;           // [rows of side] scratch: u^T G u (Dp >= 32)
 };
 
 // Number of workgroups / partial slabs the Gramian of n rows uses.

@@ -2,10 +2,15 @@
 //
 // Replaces ComputeUserLoss / ComputeLoss (ials.h:70-86 + 367-408,
 // safer2.h:85-101 + 558-596): l_u = (1/h) sum_j (x_j . u - 1)^2
-// + beta u^T G u, halved for ERM-MF / CVaR-MF / SAFER2.  One wave per user:
-// the history rows are gathered by groups of lanes (float4 per lane, one
-// row per group), dot products reduced inside the group; u^T G u reads G
-// rows coalesced from L2 with u staged in LDS.
+// + beta u^T G u, halved for ERM-MF / CVaR-MF / SAFER2.
+//
+// Dp >= 32: two passes.  quad_kernel computes q_u = u^T G u for 64 users per
+// workgroup as an MFMA product U G (U rows in LDS, G streamed by 32-row
+// slabs) with a row-dot epilogue -- G is read once per 64 users instead of
+// once per user.  loss_gather_kernel: one wave per user, eight lanes per
+// history row and eight rows in flight (8 x float4 per lane), dot products
+// reduced by DPP inside each 8-lane group.
+// Dp = 8, 16: user_loss_kernel, one wave per user, u^T G u from L2.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -80,6 +85,135 @@ __global__ void __launch_bounds__(256) user_loss_kernel(LossArgs a) {
   if (lane == 0) a.out[e] = loss;
 }
 
+
+// Sum inside groups of 8 consecutive lanes (every lane gets its group's sum).
+__device__ __forceinline__ float group8_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  return v;
+}
+
+// q[r] = u_r^T G u_r for rows row_lo .. row_lo + n_rows - 1.
+template <int NCT>
+__global__ void __launch_bounds__(256) quad_kernel(LossArgs a) {
+  constexpr int Dp = 32 * NCT, XS = Dp + 1;
+  constexpr int NTILE = 2 * NCT, MT = (NTILE + 3) / 4;
+  __shared__ float xs[64 * XS];
+  __shared__ float bs[32 * Dp];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lo = lane & 31, hi = lane >> 5;
+  const int64_t base = (int64_t)blockIdx.x * 64;
+  for (int s = tid; s < 64 * (Dp / 4); s += 256) {
+    const int rr = s / (Dp / 4), c4 = s % (Dp / 4);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (base + rr < a.n_rows)
+      v = *reinterpret_cast<const float4*>(a.U + (a.row_lo + base + rr) * Dp + 4 * c4);
+    float* d = xs + rr * XS + 4 * c4;
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  }
+  f32x16 acc[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) acc[m] = f32x16{0.f};
+  for (int c = 0; c < NCT; ++c) {
+    __syncthreads();
+    for (int s = tid; s < 32 * (Dp / 4); s += 256) {
+      const int kk = s / (Dp / 4), c4 = s % (Dp / 4);
+      *reinterpret_cast<float4*>(bs + kk * Dp + 4 * c4) =
+          *reinterpret_cast<const float4*>(a.G + (int64_t)(32 * c + kk) * Dp + 4 * c4);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int t = wave + 4 * m;
+      if (t < NTILE) {
+        const int R = t & 1, C = t >> 1;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int kk = 2 * s + hi;
+          acc[m] = mfma32(xs[(32 * R + lo) * XS + 32 * c + kk], bs[kk * Dp + 32 * C + lo], acc[m]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // (U G)[r][c] * U[r][c] in place (each element has one owner), then row sums
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int t = wave + 4 * m;
+    if (t < NTILE) {
+      const int R = t & 1, C = t >> 1;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        float* x = xs + (32 * R + acc_row(q, hi)) * XS + 32 * C + lo;
+        *x = acc[m][q] * *x;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < 64 && base + tid < a.n_rows) {
+    float qv = 0.0f;
+    const float* x = xs + tid * XS;
+    for (int c = 0; c < Dp; ++c) qv += x[c];
+    a.quad[a.row_lo + base + tid] = qv;
+  }
+}
+
+// One wave per user: 8 groups of 8 lanes, one history row per group per
+// step, each lane 8 float4 of the row (the group reads 128 contiguous
+// bytes per instruction).
+template <int Dp>
+__global__ void __launch_bounds__(256) loss_gather_kernel(LossArgs a) {
+  constexpr int WPB = 4, Q = Dp / 32;  // float4 per lane per row
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t idx = (int64_t)blockIdx.x * WPB + wave;
+  if (idx >= a.n_rows) return;
+  const int64_t e = a.row_lo + idx;
+  const int64_t p0 = a.row_ptr[e];
+  const int64_t h = a.row_ptr[e + 1] - p0;
+  if (h == 0) return;
+  const int g = lane >> 3, c = lane & 7;
+  float4 u4[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    u4[q] = *reinterpret_cast<const float4*>(a.U + e * Dp + 4 * (c + 8 * q));
+  float sq = 0.0f;
+  for (int64_t k0 = 0; k0 < h; k0 += 8) {
+    const int64_t k = k0 + g;
+    float d = 0.0f;
+    if (k < h) {
+      const int id = a.col[p0 + k];
+      const float* x = a.V + (int64_t)id * Dp;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(x + 4 * (c + 8 * q));
+        d += v.x * u4[q].x + v.y * u4[q].y + v.z * u4[q].z + v.w * u4[q].w;
+      }
+    }
+    d = group8_sum(d);
+    if (c == 0 && k < h) {
+      const float t = d - 1.0f;
+      sq = (float)((double)sq + (double)t * (double)t);
+    }
+  }
+  sq = wave_sum(sq);
+  float loss = sq / (float)h + a.beta * a.quad[e];
+  if (a.half) loss = (float)((double)loss / 2.0);
+  if (lane == 0) a.out[e] = loss;
+}
+
+template <int NCT>
+hipError_t launch2(const LossArgs& a, hipStream_t s) {
+  constexpr int Dp = 32 * NCT;
+  const unsigned nq = (unsigned)((a.n_rows + 63) / 64);
+  hipLaunchKernelGGL(quad_kernel<NCT>, dim3(nq), dim3(256), 0, s, a);
+  const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
+  hipLaunchKernelGGL(loss_gather_kernel<Dp>, dim3(nb), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 template <int Dp>
 hipError_t launch(const LossArgs& a, hipStream_t s) {
   const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
@@ -94,14 +228,14 @@ hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s) {
   switch (Dp) {
     case 8: return launch<8>(a, s);
     case 16: return launch<16>(a, s);
-    case 32: return launch<32>(a, s);
-    case 64: return launch<64>(a, s);
-    case 96: return launch<96>(a, s);
-    case 128: return launch<128>(a, s);
-    case 160: return launch<160>(a, s);
-    case 192: return launch<192>(a, s);
-    case 224: return launch<224>(a, s);
-    case 256: return launch<256>(a, s);
+    case 32: return launch2<1>(a, s);
+    case 64: return launch2<2>(a, s);
+    case 96: return launch2<3>(a, s);
+    case 128: return launch2<4>(a, s);
+    case 160: return launch2<5>(a, s);
+    case 192: return launch2<6>(a, s);
+    case 224: return launch2<7>(a, s);
+    case 256: return launch2<8>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
