@@ -5,7 +5,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 names = [r['Kernel_Name'].replace('frecsys_hip::(anonymous namespace)::', '').split('(')[0]
          .replace('void ', '') for r in rows]
-ul = [i for i, n in enumerate(names) if 'user_loss' in n]
+ul = [i for i, n in enumerate(names) if 'loss' in n]
 tot = 0.0
 for i in range(ul[-2] + 1, ul[-1] + 1):
     r = rows[i]
