@@ -31,6 +31,7 @@ using namespace frecsys_hip;
 namespace {
 
 std::string g_last_error;
+unsigned long long* g_dual_prof = nullptr;  // FRECSYS_DUAL_PROF diagnostics
 
 struct Timer {
   double total_ms = 0.0;
@@ -902,6 +903,12 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       d.other_weight = a.other_weight;
       d.fail = a.fail;
       d.debug_skip = a.debug_skip;
+      static const bool dprof = getenv("FRECSYS_DUAL_PROF") != nullptr;
+      unsigned long long*& d_prof = g_dual_prof;
+      if (dprof && !d_prof) {
+        HIP_TRY(c, hipMalloc((void**)&d_prof, sizeof(unsigned long long) * 16 * 9));
+        HIP_TRY(c, hipMemset(d_prof, 0, sizeof(unsigned long long) * 16 * 9));
+      }
       const int64_t n_hs = n_nonempty - n_dspace;
       rc = ensure(c, &c->dual_table, &c->cap_dual_table, (size_t)n_hs * 3 * c->Dp);
       if (rc) return rc;
@@ -917,6 +924,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
           d.order = a.order + lo;
           d.n_rows = hi - lo;
           d.table = c->dual_table + (size_t)(lo - n_dspace) * 3 * c->Dp;
+          d.prof = dprof ? d_prof + 16 * tiles : nullptr;
           HIP_TRY(c, launch_dual(tiles, d, c->stream));
         }
         lo = std::max(lo, hi);
@@ -944,6 +952,19 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   flush_ktimers(c);
+  if (getenv("FRECSYS_DUAL_PROF") && dual && g_dual_prof) {
+    // diagnostics: mean cycles per entity and phase of the workgroup kernel
+    unsigned long long hp[16 * 9];
+    HIP_TRY(c, hipMemcpy(hp, g_dual_prof, sizeof(hp), hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemset(g_dual_prof, 0, sizeof(hp)));
+    for (int t = 1; t <= 8; ++t) {
+      const unsigned long long n = hp[16 * t + 4];
+      if (!n) continue;
+      fprintf(stderr, "[dual-prof] side %d tiles %d n %llu cycles/entity: setup %.0f slabs %.0f chol %.0f "
+              "yz %.0f\n", side, t, n, (double)hp[16 * t] / n, (double)hp[16 * t + 1] / n,
+              (double)hp[16 * t + 2] / n, (double)hp[16 * t + 3] / n);
+    }
+  }
   if (f != none && dual && n_dspace < n_nonempty) {
     // a history-space pivot failed: the verdict is the d-space solve's
     return solve_side_impl(c, side, p, true);

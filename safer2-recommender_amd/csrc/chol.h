@@ -57,9 +57,10 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
     const float t = a[k] - ((p0 + p1) + (p2 + p3));
     const float piv = rdlane(t, k);
     ok = ok && (piv > 0.0f);
-    const float d = sqrtf(piv);
-    const float rd = 1.0f / d;
-    a[k] = (lane == k) ? d : t * rd;
+    // v_rsq_f32 (1 ulp) instead of the IEEE sqrt + divide sequences on the
+    // serial chain
+    const float rd = __builtin_amdgcn_rsqf(piv);
+    a[k] = (lane == k) ? piv * rd : t * rd;
   }
   // lanes 32..63: column j of L^-1 -> tile element (k, j), k >= j
   const int j = r;
@@ -106,7 +107,7 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
   if (wave == 0 && !(debug_skip & 2)) {
     if (!diag_factor_inv(tiles, lane) && lane == 0) flag[0] = 1;
   }
-  __syncthreads();
+  lds_barrier();
 #pragma unroll 1
   for (int p = 0; p < T; ++p) {
     const float* Tpp = tiles + tidx(p, p) * 1024;
@@ -126,7 +127,7 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
         xvec[lo] = y;  // staged; copied into bvec after the barrier
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < 32) bvec[32 * p + tid] = xvec[tid];
     if (p < T - 1) {
       const int nb = 32 * npan;
@@ -165,7 +166,7 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 
   // ---- back substitution x = L^-T y with the stored L_pp^-1 ----
@@ -183,7 +184,7 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
       pr += __shfl_xor(pr, 32);
       if (hi == 0) part[wave * 32 + lo] = pr;
     }
-    __syncthreads();
+    lds_barrier();
     if (wave == 0) {
       float r = bvec[32 * p + lo];
       for (int w = 0; w < nq; ++w) r -= part[w * 32 + lo];
@@ -193,7 +194,7 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
       for (int i = 0; i < 32; ++i) x += Tpp[sw(i, lo)] * rdlane(r, i);
       if (hi == 0) xvec[32 * p + lo] = x;
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 

@@ -40,6 +40,25 @@ __device__ __forceinline__ int acc_row(int q, int hi) {
   return (q & 3) + 8 * (q >> 2) + 4 * hi;
 }
 
+// Workgroup barrier for kernels whose waves exchange data through LDS only.
+// __syncthreads() also drains every outstanding global load of the wave
+// (s_waitcnt vmcnt(0)), which would land the one-chunk-ahead prefetches of
+// the gather loops on the critical path at each barrier; this waits for LDS
+// traffic only.  Register results of in-flight loads are waited on at
+// their first use as usual.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Same-wave LDS ordering point (no global-memory drain).
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }

@@ -96,7 +96,7 @@ __global__ void __launch_bounds__(256) dual_ldl_kernel(DualArgs a) {
     td[k] = a.tdiag[k];
     to[k] = a.toff[k];
   }
-  __syncthreads();
+  lds_barrier();
   const int64_t p = (int64_t)blockIdx.x * 256 + tid;
   if (p >= a.n_rows) return;
   const QueueRec rec = a.order[p];
@@ -225,6 +225,14 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
     bvec[tid] = tid < h ? cj : 0.0f;
   }
   if (tid == 0) flag[0] = 0;
+  unsigned long long t_prev = a.prof ? clock64() : 0;
+  auto mark = [&](int ph) {
+    if (a.prof && tid == 0) {
+      const unsigned long long t = clock64();
+      atomicAdd(a.prof + ph, t - t_prev);
+      t_prev = t;
+    }
+  };
   {  // l_k and D^-1/2 from the entity's table row
     const float* trow = a.table + (int64_t)blockIdx.x * 3 * Dp;
     for (int k = tid; k < Dp; k += NTHR) {
@@ -232,7 +240,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       dsq[k] = (a.debug_skip & 256) ? 0.5f : trow[Dp + k];
     }
   }
-  __syncthreads();
+  lds_barrier();
 
   float4 regs[NQ];
   auto load_slab = [&](int c) {
@@ -265,7 +273,8 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
 
   load_slab(0);
   store_slab();
-  __syncthreads();
+  lds_barrier();
+  mark(0);
 
   // ---- S = Z D^-1 Z^T accumulated over the 32-column slabs ----
   f32x16 acc[MT];
@@ -301,7 +310,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       }
       carry = z;
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll 4
     for (int s = 0; s < 16; ++s) {
       const float* zr = zs + (2 * s + hi) * HP;
@@ -310,7 +319,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
         if (valid[m] && !(a.debug_skip & 1)) acc[m] = mfma32(zr[aoff[m]], zr[boff[m]], acc[m]);
     }
     if (more) store_slab();
-    __syncthreads();
+    lds_barrier();
   }
 
   // ---- S = I + acc into the swizzled LDS tiles (aliasing the slabs) ----
@@ -327,8 +336,10 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
+  mark(1);
   chol_solve_tiles<TH, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
+  mark(2);
 
   // ---- v = Y^T (c.*z): the rows again, float4 per lane, 8 rows in flight ----
   {
@@ -360,13 +371,15 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       }
       *reinterpret_cast<float4*>(red + g * Dp + 4 * c4) = acc4;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < Dp) {
       float v = 0.0f;
       for (int gg = 0; gg < R; ++gg) v += red[gg * Dp + tid];
       a.out_rot[e * Dp + tid] = v;
     }
   }
+  mark(3);
+  if (a.prof && tid == 0) atomicAdd(a.prof + 4, 1ull);
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
@@ -381,11 +394,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
 // the S tiles with MFMA, factors S (chol_solve_wave) and forms Y^T (c.*z)
 // with coalesced whole-row loads.
 // ---------------------------------------------------------------------
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+__device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
 
 // chol_solve_tiles for one wave (T <= 2): x = S^-1 b, S's lower tiles in
 // LDS (swizzled), diagonal tiles become L_pp^-1.
@@ -461,7 +470,8 @@ struct WaveCfg {
   static constexpr int ZS = 32 * HP;
   static constexpr int REG = NT * 1024 > ZS ? NT * 1024 : ZS;
   static constexpr int OFF_ID = REG, OFF_C = OFF_ID + HP, OFF_B = OFF_C + HP, OFF_X = OFF_B + HP;
-  static constexpr int OFF_FLAG = OFF_X + HP;
+  static constexpr int OFF_T = OFF_X + HP;   // l_k and D^-1/2 (table row), 2 * kMaxDp
+  static constexpr int OFF_FLAG = OFF_T + 2 * kMaxDp;
   static constexpr int PW = OFF_FLAG + 4;  // floats per wave
   static constexpr size_t BYTES = (size_t)4 * PW * 4;
   static_assert(TH <= 2, "one history row per lane");
@@ -514,25 +524,37 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
     bvec[j] = j < h ? cj : 0.0f;
   }
   if (lane == 0) flag[0] = 0;
-  const float* trow = a.table + pos * 3 * Dp;  // wave-uniform
+  // the entity's l_k and D^-1/2 into LDS: the recurrence then waits on LDS
+  // only (lgkmcnt), never behind the in-flight slab prefetch (vmcnt is in
+  // order)
+  float* trow = base + C::OFF_T;
+  {
+    const float* g = a.table + pos * 3 * Dp;
+    for (int k4 = 4 * lane; k4 < 2 * Dp; k4 += 256)
+      *reinterpret_cast<float4*>(trow + k4) = *reinterpret_cast<const float4*>(g + k4);
+  }
   const float* xrow = a.Xrot + (int64_t)(id < 0 ? 0 : id) * Dp;
 
   float4 yr[8], yn[8];
+  // unconditional loads (row 0 stands in for padding rows, whose c_j = 0):
+  // no branches around the loads, so the prefetch stays in flight
   auto load = [&](int c, float4* dst) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      dst[q] = (id >= 0 && !(a.debug_skip & 32))
-                   ? *reinterpret_cast<const float4*>(xrow + 32 * c + 4 * q)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = 0; q < 8; ++q) dst[q] = *reinterpret_cast<const float4*>(xrow + 32 * c + 4 * q);
   };
-  load(0, yr);
+  load(0, yn);
+  wave_sync();
   f32x16 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = f32x16{0.f};
   float carry = 0.0f;
   for (int c = 0; c < NC; ++c) {
+    // slab c arrives (the one wait per slab), slab c+1 goes in flight, and
+    // everything below runs on registers / LDS only
+#pragma unroll
+    for (int q = 0; q < 8; ++q) yr[q] = yn[q];
     if (c + 1 < NC) load(c + 1, yn);
-    if (j < HP && !(a.debug_skip & 128)) {
+    if (j < HP) {
       float z = carry;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -547,7 +569,7 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
       carry = z;
     }
     wave_sync();
-#pragma unroll 4
+#pragma unroll
     for (int s2 = 0; s2 < 16; ++s2) {
       const float* zr = zs + (2 * s2 + hi) * HP;
 #pragma unroll
@@ -555,12 +577,10 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
         int I = 0;
         while ((I + 1) * (I + 2) / 2 <= t) ++I;
         const int J = t - I * (I + 1) / 2;
-        if (!(a.debug_skip & 1)) acc[t] = mfma32(zr[32 * I + lo], zr[32 * J + lo], acc[t]);
+        acc[t] = mfma32(zr[32 * I + lo], zr[32 * J + lo], acc[t]);
       }
     }
     wave_sync();
-#pragma unroll
-    for (int q = 0; q < 8; ++q) yr[q] = yn[q];
   }
   // S = I + acc
 #pragma unroll

@@ -107,6 +107,7 @@ struct DualArgs {
   const float* other_weight;
   unsigned long long* fail;
   int debug_skip;  // ablation only: 1 SYRK, 2/4/8/16 Cholesky parts, 64 Y^T z, 128 recurrence
+  unsigned long long* prof;  // diagnostics: per-phase cycle sums [16] (nullptr = off)
 };
 
 // Largest history-space tile count built (h_eff <= 32 * kDualMaxTiles).

@@ -239,12 +239,12 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     }
     if (tid < Dp) bacc += sl[NT * 1024 + tid];
   }
-  __syncthreads();
+  lds_barrier();
   if (nchunks > 0) {
     load_data(0);
     store_stage(0);
   }
-  __syncthreads();
+  lds_barrier();
 
   for (int c = 0; c < nchunks; ++c) {
     const int buf = c & 1;
@@ -279,7 +279,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     }
     if (more) store_stage(buf ^ 1);
     if (ring_more) ring_store(c + 2, nid, nsa, nbw);
-    __syncthreads();
+    lds_barrier();
   }
 
   if (PARTIAL) {
@@ -321,7 +321,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     if (is_u_kind(kind)) b *= us;  // rhs *= weight / history_size
     bvec[tid] = b;
   }
-  __syncthreads();
+  lds_barrier();
 
   if (grad) {
     // ---- CVaR-MF: one gradient step with the full (stale-upper) matrix ----
