@@ -15,13 +15,14 @@ fixed, so scaling is "strong".
 value = users updated per second of training wall time = N_users * K / T,
 T = max over ranks of the K-epoch wall time.  sec_per_epoch = T / K.
 
-roofline: the dominant kernel is the per-entity solve (solve_user): gather
-+ MFMA assembly + blocked Cholesky, compute-bound (arithmetic intensity
-~140 flop/B at d=256), priced against the fp32 MFMA peak (157.3 TFLOP/s).
-Algorithmic flops per entity = h*d*(d+1) + d^3/3 + 2*d^2.
-The gather-phase HBM fraction (SURVEY's graded roofline) is reported too:
-algorithmic gather bytes nnz*d*4 + nnz*4 + (N+1)*8 + N*d*4 over the same
-kernel time, against 8 TB/s.
+roofline: the dominant kernel is solve_tiled_kernel<8, false>, the d x d
+solve of the long histories (h > 256; the shorter ones take the
+history-space path): gather + MFMA assembly + blocked
+Cholesky, compute-bound, priced against the fp32 MFMA peak (157.3 TFLOP/s).
+Algorithmic flops per launch = sum over its entities of h*d*(d+1) (0 for
+the histories > 2048 rows whose SYRK the split kernel did) + d^3/3 + 2*d^2
+(SURVEY 8(d)); duration = its HIP-event time (both half-steps averaged).
+`paths` reports the same figures for the other kernels of the epoch.
 
 cpu_baseline: the CPU restatement (oracle/, "port") timing the same U
 half-step on a bounded contiguous sample of users, threads = the box's CPU
@@ -155,20 +156,57 @@ def main():
     K = args.steps
     d = args.dim
     Dp = fh.padded_dim(d)
-    su_ms, su_n = ctx.timing("solve_user")
-    si_ms, si_n = ctx.timing("solve_item")
     names = ["solve_user", "solve_item", "gramian", "user_loss", "allgather", "allreduce"]
     names += [f"{s}.{p}" for s in ("solve_user", "solve_item")
-              for p in ("dspace", "basis", "hspace", "rotate")]
+              for p in ("dspace", "split", "basis", "hspace", "rotate")]
     timers = {k: ctx.timing(k) for k in names}
-    lo, hi = ctx.shard_range(fh.SIDE_USER)
-    h = np.diff(up)[lo:hi].astype(np.float64)
-    n_own = hi - lo
-    flops = float(np.sum(h * d * (d + 1)) + n_own * (d ** 3 / 3.0 + 2.0 * d * d))
-    avg_ms = su_ms / max(su_n, 1)
-    achieved_tf = flops / (avg_ms * 1e-3) / 1e12
-    gather_bytes = float(h.sum() * d * 4 + h.sum() * 4 + (n_own + 1) * 8 + n_own * d * 4)
-    gather_gbs = gather_bytes / (avg_ms * 1e-3) / 1e9
+
+    # d-space entities of this rank (iALS: h_eff = h), split ones (> 2 * 1024)
+    dual_max = int(os.environ.get("FRECSYS_DUAL_MAX_H", "256"))
+    split_rows = int(os.environ.get("FRECSYS_SPLIT_ROWS", "1024"))
+    dual_on = os.environ.get("FRECSYS_DUAL", "1") != "0" and Dp >= 64
+    chol = d ** 3 / 3.0 + 2.0 * d * d
+    fin_flops, fin_ms, fin_n = 0.0, 0.0, 0
+    paths = {}
+    for side, ptr, name in ((fh.SIDE_USER, up, "solve_user"), (fh.SIDE_ITEM, ip, "solve_item")):
+        lo_, hi_ = ctx.shard_range(side)
+        hs = np.diff(ptr)[lo_:hi_].astype(np.float64)
+        hs = hs[hs > 0]
+        ds = hs[hs > dual_max] if dual_on else hs
+        unsplit = ds[ds <= 2 * split_rows] if split_rows > 0 else ds
+        split = ds[ds > 2 * split_rows] if split_rows > 0 else ds[:0]
+        f_fin = float(np.sum(unsplit) * d * (d + 1) + len(ds) * chol)
+        ms, n = timers[name + ".dspace"]
+        if n:
+            fin_flops += f_fin * n / max(K, 1)
+            fin_ms += ms
+            fin_n += n
+        hsp = hs[hs <= dual_max] if dual_on else hs[:0]
+        hp = 32.0 * np.ceil(hsp / 32.0)
+        paths[name] = {
+            "dspace_entities": int(len(ds)), "dspace_ms": ms / max(K, 1),
+            "dspace_tflops": f_fin / (ms / max(n, 1) * 1e-3) / 1e12 if n else None,
+            "split_rows_total": float(np.sum(split)),
+            "split_ms": timers[name + ".split"][0] / max(K, 1),
+            "split_tflops": (float(np.sum(split)) * d * (d + 1)
+                             / (timers[name + ".split"][0] / max(timers[name + ".split"][1], 1)
+                                * 1e-3) / 1e12) if timers[name + ".split"][1] else None,
+            "hspace_entities": int(len(hsp)), "hspace_ms": timers[name + ".hspace"][0] / max(K, 1),
+            # history-space algorithmic flops: h_p^2 * Dp (SYRK of S) + h_p^3 / 3
+            "hspace_tflops": (float(np.sum(hp * hp * Dp + hp ** 3 / 3.0))
+                              / (timers[name + ".hspace"][0] / max(K, 1) * 1e-3) / 1e12)
+            if timers[name + ".hspace"][1] else None,
+            "basis_ms": timers[name + ".basis"][0] / max(K, 1),
+            "rotate_ms": timers[name + ".rotate"][0] / max(K, 1),
+        }
+    avg_ms = fin_ms / max(fin_n, 1)
+    flops = fin_flops / max(fin_n / max(K, 1), 1)  # per launch
+    achieved_tf = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    n_own = ctx.shard_range(fh.SIDE_USER)[1] - ctx.shard_range(fh.SIDE_USER)[0]
+    su_ms = timers["solve_user"][0] / max(K, 1)
+    h_all = np.diff(up).astype(np.float64)
+    gather_bytes = float(h_all.sum() * d * 4 + h_all.sum() * 4 + (n_own + 1) * 8 + n_own * d * 4)
+    gather_gbs = gather_bytes / (su_ms * 1e-3) / 1e9 if su_ms > 0 else 0.0
 
     traffic = None
     traffic_src = None
@@ -176,7 +214,7 @@ def main():
     if os.path.exists(pmc) and world == 1:
         try:
             js = json.load(open(pmc))
-            traffic = js.get("solve_user_traffic_bytes")
+            traffic = js.get("dspace_traffic_bytes")
             traffic_src = js.get("source")
         except Exception:
             traffic = None
@@ -207,16 +245,17 @@ def main():
                        "n_users": nu, "n_items": ni, "nnz": nnz, "dim": d, "padded_dim": Dp,
                        "l2_reg": args.reg, "uobs_weight": args.uobs_weight,
                        "parallelism": f"entity-sharded x{world}"},
-            "u_halfstep_solve_updates_per_s": (n_own / (avg_ms * 1e-3)) * world,
+            "u_halfstep_solve_updates_per_s": (n_own / (su_ms * 1e-3)) * world if su_ms else None,
             "kernel_ms_per_epoch": {k: v[0] / max(K, 1) for k, v in timers.items()},
-            "roofline": {"bound": "mfma", "kernel": "solve_tiled_kernel<8> (solve_user)",
+            "roofline": {"bound": "mfma", "kernel": "solve_tiled_kernel<8, false> (d-space solve)",
                          "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "traffic_source": traffic_src,
                          "avg_launch_ms": avg_ms, "flops_per_launch": flops},
-            "gather_roofline": {"bound": "hbm", "achieved": gather_gbs, "peak": PEAK_HBM_GBS,
-                                "unit": "GB/s", "frac": gather_gbs / PEAK_HBM_GBS,
-                                "bytes_per_launch": gather_bytes},
+            "paths": paths,
+            "gather_roofline": {"bound": "hbm", "scope": "whole user half-step",
+                                "achieved": gather_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                "frac": gather_gbs / PEAK_HBM_GBS, "bytes_per_step": gather_bytes},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

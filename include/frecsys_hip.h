@@ -168,8 +168,9 @@ int frecsys_synchronize(frecsys_ctx* ctx);
  * streams around each launch of kernel class `what` ("solve_user",
  * "solve_item", "solve_eval", "gramian", "user_loss", "allgather",
  * "allreduce"; per solve also "<solve>.dspace" (d x d solve of the long
- * histories), "<solve>.basis" (tridiagonalisation of G + rotation of the
- * other side), "<solve>.hspace" (history-space solve), "<solve>.rotate")
+ * histories), "<solve>.split" (partial SYRKs of the longest of them),
+ * "<solve>.basis" (tridiagonalisation of G + rotation of the other side),
+ * "<solve>.hspace" (history-space solve), "<solve>.rotate")
  * since the last frecsys_timing_reset. */
 int frecsys_timing(const frecsys_ctx* ctx, const char* what, double* total_ms,
                    int64_t* launches);

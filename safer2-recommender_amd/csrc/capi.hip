@@ -855,8 +855,12 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
         rc = plan_split(c, hs, a.n_rows, heff, &ap);
         if (rc) return rc;
       }
+      if (ap.n_work > 0) {
+        const size_t k = ktimer_begin(c, pre + ".split", c->stream);
+        HIP_TRY(c, launch_split_syrk(c->Dp, ap, c->stream));
+        ktimer_end(c, k, c->stream);
+      }
       const size_t k = ktimer_begin(c, pre + ".dspace", c->stream);
-      HIP_TRY(c, launch_split_syrk(c->Dp, ap, c->stream));
       HIP_TRY(c, launch_solve(c->Dp, ap, c->stream));
       ktimer_end(c, k, c->stream);
     } else {
@@ -870,8 +874,12 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
         ap.n_rows = n_dspace;
         rc = plan_split(c, hs, n_dspace, heff, &ap);
         if (rc) return rc;
+        if (ap.n_work > 0) {
+          const size_t k = ktimer_begin(c, pre + ".split", s2);
+          HIP_TRY(c, launch_split_syrk(c->Dp, ap, s2));
+          ktimer_end(c, k, s2);
+        }
         const size_t k = ktimer_begin(c, pre + ".dspace", s2);
-        HIP_TRY(c, launch_split_syrk(c->Dp, ap, s2));
         HIP_TRY(c, launch_solve(c->Dp, ap, s2));
         ktimer_end(c, k, s2);
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));

@@ -31,13 +31,16 @@ for name in sorted(set(fetch) | set(write)):
         "fetch_bytes_per_launch": [2.0 * x for x in f],
         "write_bytes_per_launch": w,
     }
-# solve launches alternate user, item in every bench epoch (warmup included)
+# the d-space solve (roofline kernel): launches alternate user, item in
+# every bench epoch (warmup included); averaged over all launches
 for name, v in summary["kernels"].items():
-    if "solve_tiled_kernel" in name:
+    if "solve_tiled_kernel<8, false>" in name:
         tot = [a + b for a, b in zip(v["fetch_bytes_per_launch"], v["write_bytes_per_launch"])]
-        summary["solve_user_traffic_bytes"] = sum(tot[0::2]) / max(1, len(tot[0::2]))
-        summary["solve_item_traffic_bytes"] = sum(tot[1::2]) / max(1, len(tot[1::2]))
+        summary["dspace_traffic_bytes"] = sum(tot) / max(1, len(tot))
+        summary["dspace_user_traffic_bytes"] = sum(tot[0::2]) / max(1, len(tot[0::2]))
+        summary["dspace_item_traffic_bytes"] = sum(tot[1::2]) / max(1, len(tot[1::2]))
 json.dump(summary, open(sys.argv[3], "w"), indent=1)
 print(json.dumps({k: {"fetch_GB": [round(x / 1e9, 3) for x in v["fetch_bytes_per_launch"]],
                       "write_GB": [round(x / 1e9, 3) for x in v["write_bytes_per_launch"]]}
-                  for k, v in summary["kernels"].items() if "solve" in k or "loss" in k}, indent=1))
+                  for k, v in summary["kernels"].items()
+                  if "solve" in k or "loss" in k or "dual" in k}, indent=1))
