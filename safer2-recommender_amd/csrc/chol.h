@@ -103,7 +103,8 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
                                                  float* part, int* flag, int tid,
                                                  int debug_skip) {
   static_assert(T - 1 < NW || T == 1, "back substitution needs one wave per tile");
-  const int lane = tid & 63, wave = tid >> 6, lo = lane & 31, hi = lane >> 5;
+  const int lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (wave == 0 && !(debug_skip & 2)) {
     if (!diag_factor_inv(tiles, lane) && lane == 0) flag[0] = 1;
   }

@@ -191,7 +191,8 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
   float* part = smem + C::OFF_PART;
   int* flag = reinterpret_cast<int*>(smem + C::OFF_FLAG);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform branches
   const int lo = lane & 31, hi = lane >> 5;
   const int kind = a.kind;
   const bool vk = is_v_kind(kind), uk = is_u_kind(kind);
@@ -311,12 +312,17 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       carry = z;
     }
     lds_barrier();
-#pragma unroll 4
-    for (int s = 0; s < 16; ++s) {
-      const float* zr = zs + (2 * s + hi) * HP;
+    if (!(a.debug_skip & 1)) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
-        if (valid[m] && !(a.debug_skip & 1)) acc[m] = mfma32(zr[aoff[m]], zr[boff[m]], acc[m]);
+      for (int m = 0; m < MT; ++m) {
+        if (valid[m]) {  // wave-uniform
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            const float* zr = zs + (2 * s + hi) * HP;
+            acc[m] = mfma32(zr[aoff[m]], zr[boff[m]], acc[m]);
+          }
+        }
+      }
     }
     if (more) store_slab();
     lds_barrier();

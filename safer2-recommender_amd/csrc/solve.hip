@@ -98,7 +98,8 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
   int* ring_id = reinterpret_cast<int*>(smem + C::OFF_ID);
   int* flag = reinterpret_cast<int*>(smem + C::OFF_FLAG);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform branches
   const int lo = lane & 31, hi = lane >> 5;
   const int kind = a.kind;
   const bool vk = is_v_kind(kind);
@@ -137,9 +138,12 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     if (k < k1) {
       id = a.col[p0 + virt_pos(k, h)];
       if (vk) {
+        // rows are staged pre-scaled by sa (the factor column sqrt(w) * cp_v,
+        // safer2.h:192); the rhs weight w (safer2.h:190) is then applied as
+        // w / sa to the scaled row
         const float nu = a.other_weight[id];
-        sa = sqrtf(nu);            // factor col = sqrt(w) * cp_v, safer2.h:192
-        bw = (k < h) ? nu : 0.0f;  // rhs += w * cp_v, safer2.h:190
+        sa = sqrtf(nu);
+        bw = (k < h && sa > 0.0f) ? nu / sa : 0.0f;
       } else {
         sa = 1.0f;
         bw = 1.0f;
@@ -166,12 +170,23 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
       }
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf, int c) {
     float* st = stage + buf * R * Dp;
+    const int slot = c % kRing;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int sidx = tid + q * NTHR;
-      if (NSLOT % NTHR == 0 || sidx < NSLOT) *reinterpret_cast<float4*>(st + 4 * sidx) = regs[q];
+      if (NSLOT % NTHR == 0 || sidx < NSLOT) {
+        float4 v = regs[q];
+        if (vk) {
+          const float sc = ring_sa[slot * R + sidx / (Dp / 4)];
+          v.x *= sc;
+          v.y *= sc;
+          v.z *= sc;
+          v.w *= sc;
+        }
+        *reinterpret_cast<float4*>(st + 4 * sidx) = v;
+      }
     }
   };
 
@@ -242,7 +257,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
   lds_barrier();
   if (nchunks > 0) {
     load_data(0);
-    store_stage(0);
+    store_stage(0, 0);
   }
   lds_barrier();
 
@@ -256,20 +271,17 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     if (ring_more) ring_load(c + 2, nid, nsa, nbw);
     const float* st = stage + buf * R * Dp;
     const int slot = c % kRing;
-#pragma unroll 4
-    for (int s = 0; s < R / 2; ++s) {
-      const float* rowp = st + (2 * s + hi) * Dp;
-      const float sa = vk ? ring_sa[slot * R + 2 * s + hi] : 1.0f;
+    // tile-outer, row-pair-inner: one wave-uniform branch per tile and the
+    // operand reads free to run ahead of the MFMAs
+    if (!(a.debug_skip & 1)) {
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        if (valid[m] && !(a.debug_skip & 1)) {
-          float fa = rowp[aoff[m]];
-          float fb = rowp[boff[m]];
-          if (vk) {
-            fa *= sa;
-            fb *= sa;
+        if (valid[m]) {
+#pragma unroll
+          for (int s = 0; s < R / 2; ++s) {
+            const float* rowp = st + (2 * s + hi) * Dp;
+            acc[m] = mfma32(rowp[aoff[m]], rowp[boff[m]], acc[m]);
           }
-          acc[m] = mfma32(fa, fb, acc[m]);
         }
       }
     }
@@ -277,7 +289,7 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
 #pragma unroll 4
       for (int r = 0; r < R; ++r) bacc += ring_bw[slot * R + r] * st[r * Dp + tid];
     }
-    if (more) store_stage(buf ^ 1);
+    if (more) store_stage(buf ^ 1, c + 1);
     if (ring_more) ring_store(c + 2, nid, nsa, nbw);
     lds_barrier();
   }
