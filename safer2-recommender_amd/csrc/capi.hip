@@ -888,9 +888,6 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       rc = prepare_basis(c, other, a.X, c->stream);
       if (rc) return rc;
       ktimer_end(c, k, c->stream);
-      rc = ensure(c, &c->out_rot[side], &c->cap_out_rot[side],
-                  (size_t)std::max<int64_t>(c->n[side], 1) * c->Dp);
-      if (rc) return rc;
       DualArgs d{};
       d.kind = kind;
       d.quirk = c->quirks;
@@ -900,7 +897,6 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       d.tdiag = c->tri[other];
       d.toff = c->tri[other] + c->Dp;
       d.n_other = a.n_other;
-      d.out_rot = c->out_rot[side];
       d.reg = a.reg;
       d.reg_exp = a.reg_exp;
       d.w = a.w;
@@ -918,12 +914,17 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
         HIP_TRY(c, hipMemset(d_prof, 0, sizeof(unsigned long long) * 16 * 9));
       }
       const int64_t n_hs = n_nonempty - n_dspace;
-      rc = ensure(c, &c->dual_table, &c->cap_dual_table, (size_t)n_hs * 3 * c->Dp);
+      const size_t n_blk = (size_t)((n_hs + 63) / 64) * 64;  // position-blocked buffers
+      rc = ensure(c, &c->dual_table, &c->cap_dual_table, n_blk * 3 * c->Dp);
       if (rc) return rc;
+      rc = ensure(c, &c->out_rot[side], &c->cap_out_rot[side], n_blk * c->Dp);
+      if (rc) return rc;
+      d.out_rot = c->out_rot[side];
       k = ktimer_begin(c, pre + ".hspace", c->stream);
       d.order = a.order + n_dspace;
       d.n_rows = n_hs;
       d.table = c->dual_table;
+      d.pos0 = 0;
       HIP_TRY(c, launch_dual_ldl(d, c->stream));
       int64_t lo = n_dspace;
       for (int tiles = kDualMaxTiles; tiles >= 1 && lo < n_nonempty; --tiles) {
@@ -931,7 +932,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
         if (hi > lo) {
           d.order = a.order + lo;
           d.n_rows = hi - lo;
-          d.table = c->dual_table + (size_t)(lo - n_dspace) * 3 * c->Dp;
+          d.pos0 = lo - n_dspace;
           d.prof = dprof ? d_prof + 16 * tiles : nullptr;
           HIP_TRY(c, launch_dual(tiles, d, c->stream));
         }
@@ -939,12 +940,12 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       }
       d.order = a.order + n_dspace;
       d.n_rows = n_hs;
-      d.table = c->dual_table;
+      d.pos0 = 0;
       HIP_TRY(c, launch_dual_sweep(d, c->stream));
       ktimer_end(c, k, c->stream);
       k = ktimer_begin(c, pre + ".rotate", c->stream);
       HIP_TRY(c, launch_rot_gemm(c->out_rot[side], a.order + n_dspace, 0, n_nonempty - n_dspace,
-                                 c->q[other], 1, a.out, c->Dp, c->stream));
+                                 c->q[other], 1, a.out, c->Dp, c->stream, 1));
       ktimer_end(c, k, c->stream);
       if (n_dspace > 0) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     }

@@ -55,7 +55,7 @@ struct DualCfg {
   static constexpr int STG = HP * SROW;
   static constexpr int ZS = 32 * HP;                // k-major scaled Z slab
   static constexpr int TILES = NT * 1024;
-  static constexpr int LOOP = ((STG + ZS + 3) / 4) * 4;
+  static constexpr int LOOP = ((2 * STG + ZS + 3) / 4) * 4;  // two stages + Z
   static constexpr int REGION0 = TILES > LOOP ? TILES : LOOP;
   static constexpr int OFF_L = REGION0;             // l_k
   static constexpr int OFF_DS = OFF_L + kMaxDp;     // D^-1/2
@@ -102,33 +102,21 @@ __global__ void __launch_bounds__(256) dual_ldl_kernel(DualArgs a) {
   const QueueRec rec = a.order[p];
   float mu, lam, omega;
   dual_scalars(a, rec.entity, rec.h, mu, lam, omega);
-  float* lrow = a.table + p * 3 * Dp;
-  float* srow = lrow + Dp;
-  float* irow = srow + Dp;
   // l_k = b_k / d_{k-1}, d_k = a_k - l_k b_k (a = mu*diag + lam, b = mu*sub);
-  // stored by float4 (the rows of neighbouring lanes are 3*Dp floats apart)
-  float dprev = 1.0f, r = 0.0f;
+  // position-blocked table: consecutive lanes write consecutive floats
+  const int64_t pp = a.pos0 + p;
+  float r = 0.0f;
   bool ok = true;
-  for (int k4 = 0; k4 < Dp; k4 += 4) {
-    float lv[4], sv[4], iv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = k4 + u;
-      const float b = k > 0 ? mu * to[k - 1] : 0.0f;
-      const float l = b * r;
-      const float dk = (mu * td[k] + lam) - l * b;
-      ok = ok && (dk > 0.0f);
-      r = __builtin_amdgcn_rcpf(dk);
-      lv[u] = l;
-      sv[u] = __builtin_amdgcn_rsqf(dk);
-      iv[u] = r;
-      dprev = dk;
-    }
-    *reinterpret_cast<float4*>(lrow + k4) = make_float4(lv[0], lv[1], lv[2], lv[3]);
-    *reinterpret_cast<float4*>(srow + k4) = make_float4(sv[0], sv[1], sv[2], sv[3]);
-    *reinterpret_cast<float4*>(irow + k4) = make_float4(iv[0], iv[1], iv[2], iv[3]);
+  for (int k = 0; k < Dp; ++k) {
+    const float b = k > 0 ? mu * to[k - 1] : 0.0f;
+    const float l = b * r;
+    const float dk = (mu * td[k] + lam) - l * b;
+    ok = ok && (dk > 0.0f);
+    r = __builtin_amdgcn_rcpf(dk);
+    a.table[blk_t(pp, 0, k, Dp)] = l;
+    a.table[blk_t(pp, 1, k, Dp)] = __builtin_amdgcn_rsqf(dk);
+    a.table[blk_t(pp, 2, k, Dp)] = r;
   }
-  (void)dprev;
   if (!ok) atomicMin(a.fail, (unsigned long long)(rec.entity + 1));
 }
 
@@ -137,39 +125,21 @@ __global__ void __launch_bounds__(256) dual_sweep_kernel(DualArgs a) {
   const int Dp = a.Dp;
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (p >= a.n_rows) return;
-  const int64_t e = a.order[p].entity;
-  float* v = a.out_rot + e * Dp;
-  const float* lrow = a.table + p * 3 * Dp;
-  const float* irow = lrow + 2 * Dp;
+  const int64_t pp = a.pos0 + p;
   float u = 0.0f;
-  for (int k4 = 0; k4 < Dp; k4 += 4) {  // L u = v, then D^-1
-    float4 vv = *reinterpret_cast<const float4*>(v + k4);
-    const float4 ll = *reinterpret_cast<const float4*>(lrow + k4);
-    const float4 ii = *reinterpret_cast<const float4*>(irow + k4);
-    u = vv.x - ll.x * u;
-    vv.x = u * ii.x;
-    u = vv.y - ll.y * u;
-    vv.y = u * ii.y;
-    u = vv.z - ll.z * u;
-    vv.z = u * ii.z;
-    u = vv.w - ll.w * u;
-    vv.w = u * ii.w;
-    *reinterpret_cast<float4*>(v + k4) = vv;
+#pragma unroll 8
+  for (int k = 0; k < Dp; ++k) {  // L u = v, then D^-1
+    const int64_t iv = blk_v(pp, k, Dp);
+    u = a.out_rot[iv] - a.table[blk_t(pp, 0, k, Dp)] * u;
+    a.out_rot[iv] = u * a.table[blk_t(pp, 2, k, Dp)];
   }
-  float x = 0.0f, lnext = 0.0f;  // L^T x = D^-1 u, l_Dp = 0
-  for (int k4 = Dp - 4; k4 >= 0; k4 -= 4) {
-    float4 ww = *reinterpret_cast<const float4*>(v + k4);
-    const float4 ll = *reinterpret_cast<const float4*>(lrow + k4);
-    x = ww.w - lnext * x;
-    ww.w = x;
-    x = ww.z - ll.w * x;
-    ww.z = x;
-    x = ww.y - ll.z * x;
-    ww.y = x;
-    x = ww.x - ll.y * x;
-    ww.x = x;
-    lnext = ll.x;
-    *reinterpret_cast<float4*>(v + k4) = ww;
+  float x = 0.0f;
+#pragma unroll 8
+  for (int k = Dp - 1; k >= 0; --k) {  // L^T x = D^-1 u
+    const float l1 = k + 1 < Dp ? a.table[blk_t(pp, 0, k + 1, Dp)] : 0.0f;
+    const int64_t iv = blk_v(pp, k, Dp);
+    x = a.out_rot[iv] - l1 * x;
+    a.out_rot[iv] = x;
   }
 }
 
@@ -181,7 +151,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tiles = smem;
   float* stage = smem;
-  float* zs = smem + C::STG;
+  float* zs = smem + 2 * C::STG;
   float* lsub = smem + C::OFF_L;
   float* dsq = smem + C::OFF_DS;
   float* cvec = smem + C::OFF_C;
@@ -235,16 +205,18 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
     }
   };
   {  // l_k and D^-1/2 from the entity's table row
-    const float* trow = a.table + (int64_t)blockIdx.x * 3 * Dp;
+    const int64_t pp = a.pos0 + blockIdx.x;
     for (int k = tid; k < Dp; k += NTHR) {
-      lsub[k] = (a.debug_skip & 256) ? 0.5f : trow[k];
-      dsq[k] = (a.debug_skip & 256) ? 0.5f : trow[Dp + k];
+      lsub[k] = (a.debug_skip & 256) ? 0.5f : a.table[blk_t(pp, 0, k, Dp)];
+      dsq[k] = (a.debug_skip & 256) ? 0.5f : a.table[blk_t(pp, 1, k, Dp)];
     }
   }
   lds_barrier();
 
-  float4 regs[NQ];
-  auto load_slab = [&](int c) {
+  // two register sets and two LDS stages: slab c+2's loads are issued when
+  // slab c starts and stored at the end of slab c+1 (two slabs of cover)
+  float4 ra[NQ], rb[NQ];
+  auto load_slab = [&](int c, float4 (&regs)[NQ]) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int s = tid + q * NTHR;
@@ -257,13 +229,13 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       }
     }
   };
-  auto store_slab = [&]() {
+  auto store_slab = [&](const float4 (&regs)[NQ], int buf) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int s = tid + q * NTHR;
       if ((HP * 8) % NTHR == 0 || s < HP * 8) {
         const int r = s >> 3, c4 = s & 7;
-        float* d = stage + r * SROW + 4 * c4;
+        float* d = stage + buf * C::STG + r * SROW + 4 * c4;
         d[0] = regs[q].x;
         d[1] = regs[q].y;
         d[2] = regs[q].z;
@@ -272,8 +244,9 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
     }
   };
 
-  load_slab(0);
-  store_slab();
+  load_slab(0, ra);
+  if (NC > 1) load_slab(1, rb);
+  store_slab(ra, 0);
   lds_barrier();
   mark(0);
 
@@ -294,11 +267,11 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
   }
   float carry = 0.0f;
   const float cj = tid < HP ? cvec[tid] : 0.0f;
-  for (int c = 0; c < NC; ++c) {
-    const bool more = c + 1 < NC;
-    if (more) load_slab(c + 1);
+  // slab c: in LDS stage c&1; slab c+1 in the other register set
+  auto slab_step = [&](int c, float4 (&mine)[NQ], float4 (&next)[NQ]) {
+    if (c + 2 < NC) load_slab(c + 2, mine);
     if (tid < HP && !(a.debug_skip & 128)) {
-      const float* yrow = stage + tid * SROW;
+      const float* yrow = stage + (c & 1) * C::STG + tid * SROW;
       float y[32];
 #pragma unroll
       for (int kk = 0; kk < 32; ++kk) y[kk] = yrow[kk];
@@ -324,8 +297,12 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
         }
       }
     }
-    if (more) store_slab();
+    if (c + 1 < NC) store_slab(next, (c + 1) & 1);
     lds_barrier();
+  };
+  for (int c = 0; c < NC; c += 2) {
+    slab_step(c, ra, rb);
+    if (c + 1 < NC) slab_step(c + 1, rb, ra);
   }
 
   // ---- S = I + acc into the swizzled LDS tiles (aliasing the slabs) ----
@@ -381,7 +358,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
     if (tid < Dp) {
       float v = 0.0f;
       for (int gg = 0; gg < R; ++gg) v += red[gg * Dp + tid];
-      a.out_rot[e * Dp + tid] = v;
+      a.out_rot[blk_v(a.pos0 + blockIdx.x, tid, Dp)] = v;
     }
   }
   mark(3);
@@ -535,9 +512,9 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   // order)
   float* trow = base + C::OFF_T;
   {
-    const float* g = a.table + pos * 3 * Dp;
-    for (int k4 = 4 * lane; k4 < 2 * Dp; k4 += 256)
-      *reinterpret_cast<float4*>(trow + k4) = *reinterpret_cast<const float4*>(g + k4);
+    const int64_t pp = a.pos0 + pos;
+    for (int k = lane; k < 2 * Dp; k += 64)
+      trow[k] = a.table[blk_t(pp, k >= Dp, k >= Dp ? k - Dp : k, Dp)];
   }
   const float* xrow = a.Xrot + (int64_t)(id < 0 ? 0 : id) * Dp;
 
@@ -629,7 +606,13 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
       }
     }
   }
-  if (4 * lane < Dp) *reinterpret_cast<float4*>(a.out_rot + e * Dp + 4 * lane) = v4;
+  if (4 * lane < Dp) {
+    const int64_t pp = a.pos0 + pos;
+    a.out_rot[blk_v(pp, 4 * lane + 0, Dp)] = v4.x;
+    a.out_rot[blk_v(pp, 4 * lane + 1, Dp)] = v4.y;
+    a.out_rot[blk_v(pp, 4 * lane + 2, Dp)] = v4.z;
+    a.out_rot[blk_v(pp, 4 * lane + 3, Dp)] = v4.w;
+  }
   if (lane == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 

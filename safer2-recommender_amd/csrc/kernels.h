@@ -98,8 +98,14 @@ struct DualArgs {
   const float* tdiag;       // [Dp] diagonal of T
   const float* toff;        // [Dp] T(k+1, k)
   int64_t n_other;
-  float* out_rot;           // Y^T z per solved row (row = entity), ld Dp
-  float* table;             // [n_rows][3][Dp]: l_k, D^-1/2, D^-1 of mu*T + lam*I
+  // position-blocked buffers (64 positions per block, k-major inside a
+  // block: every access by consecutive positions is coalesced), position =
+  // pos0 + index in this launch's order slice:
+  //   out_rot[blk][k][64]     Y^T (c.*z), then x'
+  //   table[blk][3][Dp][64]   l_k, D^-1/2, D^-1 of mu*T + lam*I
+  float* out_rot;
+  float* table;
+  int64_t pos0;
   float reg, reg_exp, w, alpha;
   int lambda_is_reg;
   const float* entity_weight;
@@ -134,9 +140,19 @@ hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, flo
 // Q = H_0 H_1 ... H_{Dp-3} from the reflectors, row-major Dp x Dp.
 hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s);
 // Y[row] = X[row] * (trans ? Q^T : Q) for rows r0..r0+n-1, or for the
-// entities rows[0..n) when rows != nullptr.  X, Y: ld Dp.
+// entities rows[0..n) when rows != nullptr.  Y: ld Dp; X: ld Dp, or with
+// x_blocked the position-blocked layout of DualArgs::out_rot (X row r =
+// position r).
 hipError_t launch_rot_gemm(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
-                           const float* Q, int trans, float* Y, int Dp, hipStream_t s);
+                           const float* Q, int trans, float* Y, int Dp, hipStream_t s,
+                           int x_blocked = 0);
+
+__host__ __device__ inline int64_t blk_v(int64_t p, int k, int Dp) {
+  return ((p >> 6) * Dp + k) * 64 + (p & 63);
+}
+__host__ __device__ inline int64_t blk_t(int64_t p, int j, int k, int Dp) {
+  return ((p >> 6) * 3 * Dp + j * Dp + k) * 64 + (p & 63);
+}
 hipError_t launch_gramian(int Dp, const GramArgs& a, hipStream_t s);
 hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s);
 hipError_t launch_zero_gram(int Dp, float* G, hipStream_t s);

@@ -241,7 +241,8 @@ __global__ void __launch_bounds__(256)
 template <int NCT>
 __global__ void __launch_bounds__(256)
     rot_gemm_kernel(const float* __restrict__ X, const QueueRec* __restrict__ rows, int64_t r0,
-                    int64_t n, const float* __restrict__ Q, int trans, float* __restrict__ Y) {
+                    int64_t n, const float* __restrict__ Q, int trans, float* __restrict__ Y,
+                    int x_blocked) {
   constexpr int Dp = 32 * NCT, XS = Dp + 1;
   constexpr int NTILE = 2 * NCT, MT = (NTILE + 3) / 4;
   __shared__ float xs[64 * XS];
@@ -254,16 +255,21 @@ __global__ void __launch_bounds__(256)
     rid[tid] = r < n ? (rows ? (int64_t)rows[r].entity : r0 + r) : -1;
   }
   __syncthreads();
-  for (int s = tid; s < 64 * (Dp / 4); s += 256) {
-    const int rr = s / (Dp / 4), c4 = s % (Dp / 4);
-    const int64_t id = rid[rr];
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (id >= 0) v = *reinterpret_cast<const float4*>(X + id * Dp + 4 * c4);
-    float* d = xs + rr * XS + 4 * c4;
-    d[0] = v.x;
-    d[1] = v.y;
-    d[2] = v.z;
-    d[3] = v.w;
+  if (x_blocked) {  // rows = positions base .. base+63 = one 64-position block
+    const float* xb = X + base * Dp;
+    for (int s = tid; s < 64 * Dp; s += 256) xs[(s & 63) * XS + (s >> 6)] = xb[s];
+  } else {
+    for (int s = tid; s < 64 * (Dp / 4); s += 256) {
+      const int rr = s / (Dp / 4), c4 = s % (Dp / 4);
+      const int64_t id = rid[rr];
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (id >= 0) v = *reinterpret_cast<const float4*>(X + id * Dp + 4 * c4);
+      float* d = xs + rr * XS + 4 * c4;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
   }
   f32x16 acc[MT];
 #pragma unroll
@@ -316,9 +322,10 @@ __global__ void __launch_bounds__(256)
 
 template <int NCT>
 hipError_t launch_rot(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
-                      const float* Q, int trans, float* Y, hipStream_t s) {
+                      const float* Q, int trans, float* Y, hipStream_t s, int xb) {
   const unsigned nb = (unsigned)((n + 63) / 64);
-  hipLaunchKernelGGL(rot_gemm_kernel<NCT>, dim3(nb), dim3(256), 0, s, X, rows, r0, n, Q, trans, Y);
+  hipLaunchKernelGGL(rot_gemm_kernel<NCT>, dim3(nb), dim3(256), 0, s, X, rows, r0, n, Q, trans, Y,
+                     xb);
   return hipGetLastError();
 }
 
@@ -339,16 +346,17 @@ hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hi
 }
 
 hipError_t launch_rot_gemm(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
-                           const float* Q, int trans, float* Y, int Dp, hipStream_t s) {
+                           const float* Q, int trans, float* Y, int Dp, hipStream_t s,
+                           int x_blocked) {
   if (n <= 0) return hipSuccess;
   switch (Dp) {
-    case 64: return launch_rot<2>(X, rows, r0, n, Q, trans, Y, s);
-    case 96: return launch_rot<3>(X, rows, r0, n, Q, trans, Y, s);
-    case 128: return launch_rot<4>(X, rows, r0, n, Q, trans, Y, s);
-    case 160: return launch_rot<5>(X, rows, r0, n, Q, trans, Y, s);
-    case 192: return launch_rot<6>(X, rows, r0, n, Q, trans, Y, s);
-    case 224: return launch_rot<7>(X, rows, r0, n, Q, trans, Y, s);
-    case 256: return launch_rot<8>(X, rows, r0, n, Q, trans, Y, s);
+    case 64: return launch_rot<2>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
+    case 96: return launch_rot<3>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
+    case 128: return launch_rot<4>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
+    case 160: return launch_rot<5>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
+    case 192: return launch_rot<6>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
+    case 224: return launch_rot<7>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
+    case 256: return launch_rot<8>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
     default: return hipErrorInvalidValue;
   }
 }
