@@ -84,7 +84,9 @@ struct frecsys_ctx {
   // solve of the long histories, the basis of each side's Gramian, the
   // rotated copy of each side, and the solved rows in the rotated basis
   hipStream_t stream2 = nullptr;
+  hipStream_t stream3 = nullptr;  // second lane of history-space buckets
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork3 = nullptr, ev_join3 = nullptr;
   float* q[2] = {nullptr, nullptr};      // Dp x Dp
   float* tri[2] = {nullptr, nullptr};    // [2 * Dp]: diagonal, subdiagonal
   float* refl[2] = {nullptr, nullptr};   // Dp x Dp reflectors + [Dp] tau
@@ -471,14 +473,21 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   };
   if (hipSetDevice(c->device) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_NO_DEVICE, "hipSetDevice failed"));
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
-    return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed"));
+  {  // the history-space chain (basis -> buckets) runs on the high-priority stream
+    int lo_pri = 0, hi_pri = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri);
+    if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi_pri) != hipSuccess)
+      return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed"));
+  }
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_HIP, "hipEventCreate failed"));
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
-    return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed (stream2)"));
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork3, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join3, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed (stream2/3)"));
   if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H")) c->dual_max_h = atoi(v);
   if (const char* v = getenv("FRECSYS_DUAL_SERIAL")) c->dual_serial = atoi(v);
@@ -535,6 +544,12 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (c->d_slabs) (void)hipFree(c->d_slabs);
   for (auto& p : c->pending) c->event_pool.insert(c->event_pool.end(), {p.a, p.b});
   for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
+  if (c->ev_fork3) (void)hipEventDestroy(c->ev_fork3);
+  if (c->ev_join3) (void)hipEventDestroy(c->ev_join3);
+  if (c->stream3) {
+    (void)hipStreamSynchronize(c->stream3);
+    (void)hipStreamDestroy(c->stream3);
+  }
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->stream2) {
@@ -866,28 +881,31 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
     } else {
       // d-space solve of the long histories on stream2, concurrently with
       // the basis change + history-space solve of the rest on stream
+      // the basis (one-workgroup tridiagonalisation first) is queued before
+      // the d-space kernels so its workgroup is not left waiting for a CU
+      // behind them; stream2 waits only for what preceded the fork
       hipStream_t s2 = c->dual_serial ? c->stream : c->stream2;
+      if (n_dspace > 0) HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
+      size_t k = ktimer_begin(c, pre + ".basis", c->stream);
+      rc = prepare_basis(c, other, a.X, c->stream);
+      if (rc) return rc;
+      ktimer_end(c, k, c->stream);
       if (n_dspace > 0) {
-        HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
         SolveArgs ap = a;
         ap.n_rows = n_dspace;
         rc = plan_split(c, hs, n_dspace, heff, &ap);
         if (rc) return rc;
         if (ap.n_work > 0) {
-          const size_t k = ktimer_begin(c, pre + ".split", s2);
+          const size_t k2 = ktimer_begin(c, pre + ".split", s2);
           HIP_TRY(c, launch_split_syrk(c->Dp, ap, s2));
-          ktimer_end(c, k, s2);
+          ktimer_end(c, k2, s2);
         }
-        const size_t k = ktimer_begin(c, pre + ".dspace", s2);
+        const size_t k2 = ktimer_begin(c, pre + ".dspace", s2);
         HIP_TRY(c, launch_solve(c->Dp, ap, s2));
-        ktimer_end(c, k, s2);
+        ktimer_end(c, k2, s2);
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
       }
-      size_t k = ktimer_begin(c, pre + ".basis", c->stream);
-      rc = prepare_basis(c, other, a.X, c->stream);
-      if (rc) return rc;
-      ktimer_end(c, k, c->stream);
       DualArgs d{};
       d.kind = kind;
       d.quirk = c->quirks;
@@ -926,6 +944,13 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       d.table = c->dual_table;
       d.pos0 = 0;
       HIP_TRY(c, launch_dual_ldl(d, c->stream));
+      // buckets in two lanes (the long ones on stream, the short ones on
+      // stream3) so one bucket's tail and resource shape overlap another's
+      const bool two_lanes = !c->dual_serial;
+      if (two_lanes) {
+        HIP_TRY(c, hipEventRecord(c->ev_fork3, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream3, c->ev_fork3, 0));
+      }
       int64_t lo = n_dspace;
       for (int tiles = kDualMaxTiles; tiles >= 1 && lo < n_nonempty; --tiles) {
         const int64_t hi = std::min(n_nonempty, first_le(32 * (tiles - 1)));
@@ -934,9 +959,14 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
           d.n_rows = hi - lo;
           d.pos0 = lo - n_dspace;
           d.prof = dprof ? d_prof + 16 * tiles : nullptr;
-          HIP_TRY(c, launch_dual(tiles, d, c->stream));
+          hipStream_t ls = (two_lanes && tiles <= 4) ? c->stream3 : c->stream;
+          HIP_TRY(c, launch_dual(tiles, d, ls));
         }
         lo = std::max(lo, hi);
+      }
+      if (two_lanes) {
+        HIP_TRY(c, hipEventRecord(c->ev_join3, c->stream3));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join3, 0));
       }
       d.order = a.order + n_dspace;
       d.n_rows = n_hs;
