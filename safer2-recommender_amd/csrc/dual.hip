@@ -48,14 +48,15 @@ template <int TH>
 struct DualCfg {
   static constexpr int HP = 32 * TH;                // padded history rows
   static constexpr int NT = TH * (TH + 1) / 2;      // lower tiles of S
-  static constexpr int NW = (TH <= 2) ? 4 : 8;
+  static constexpr int NW = (TH <= 4) ? 4 : 8;      // more, smaller workgroups per CU
   static constexpr int NTHR = NW * 64;
   static constexpr int MT = (NT + NW - 1) / NW;
   static constexpr int SROW = 33;                   // slab row stride
   static constexpr int STG = HP * SROW;
   static constexpr int ZS = 32 * HP;                // k-major scaled Z slab
   static constexpr int TILES = NT * 1024;
-  static constexpr int LOOP = ((2 * STG + ZS + 3) / 4) * 4;  // two stages + Z
+  static constexpr int NSTAGE = (TH <= 4) ? 1 : 2;  // LDS stages for the slab prefetch
+  static constexpr int LOOP = ((NSTAGE * STG + ZS + 3) / 4) * 4;
   static constexpr int REGION0 = TILES > LOOP ? TILES : LOOP;
   static constexpr int OFF_L = REGION0;             // l_k
   static constexpr int OFF_DS = OFF_L + kMaxDp;     // D^-1/2
@@ -151,7 +152,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tiles = smem;
   float* stage = smem;
-  float* zs = smem + 2 * C::STG;
+  float* zs = smem + C::NSTAGE * C::STG;
   float* lsub = smem + C::OFF_L;
   float* dsq = smem + C::OFF_DS;
   float* cvec = smem + C::OFF_C;
@@ -235,7 +236,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       const int s = tid + q * NTHR;
       if ((HP * 8) % NTHR == 0 || s < HP * 8) {
         const int r = s >> 3, c4 = s & 7;
-        float* d = stage + buf * C::STG + r * SROW + 4 * c4;
+        float* d = stage + (buf % C::NSTAGE) * C::STG + r * SROW + 4 * c4;
         d[0] = regs[q].x;
         d[1] = regs[q].y;
         d[2] = regs[q].z;
@@ -271,7 +272,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
   auto slab_step = [&](int c, float4 (&mine)[NQ], float4 (&next)[NQ]) {
     if (c + 2 < NC) load_slab(c + 2, mine);
     if (tid < HP && !(a.debug_skip & 128)) {
-      const float* yrow = stage + (c & 1) * C::STG + tid * SROW;
+      const float* yrow = stage + ((c & 1) % C::NSTAGE) * C::STG + tid * SROW;
       float y[32];
 #pragma unroll
       for (int kk = 0; kk < 32; ++kk) y[kk] = yrow[kk];
