@@ -47,7 +47,7 @@ struct TiledCfg {
   static constexpr int NW = (T <= 2) ? 4 : 8;       // waves per workgroup
   static constexpr int NTHR = NW * 64;
   static constexpr int MT = (NT + NW - 1) / NW;     // tiles per wave (max)
-  static constexpr int R = (T <= 2) ? 16 : 32;      // rows per staged chunk
+  static constexpr int R = (T <= 2) ? 16 : (T >= 8 ? 64 : 32);  // rows per staged chunk
   static constexpr int NSLOT = R * Dp / 4;          // float4 per chunk
   static constexpr int NQ = (NSLOT + NTHR - 1) / NTHR;
   // LDS carve (floats); every offset a multiple of 4 floats (16 B).
