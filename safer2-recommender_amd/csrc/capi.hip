@@ -96,6 +96,12 @@ struct frecsys_ctx {
   size_t cap_out_rot[3] = {0, 0, 0};
   float* dual_table = nullptr;  // [entities][3][Dp] LDL^T factors
   size_t cap_dual_table = 0;
+  // wide dims (Dp = 512 / 1024): tridiagonalisation work, d-space workspace
+  float* tri_work = nullptr;
+  size_t cap_tri_work = 0;
+  float* wide_ws = nullptr;      // [wide batch][wide_slot_floats(Dp)]
+  size_t cap_wide_ws = 0;
+  int64_t wide_ws_mb = 4096;     // FRECSYS_WIDE_WS_MB: workspace budget
   // long-history split of the d-space solve
   int split_rows = 1024;         // rows per partial SYRK (FRECSYS_SPLIT_ROWS, 0 = off)
   std::vector<int2> h_split;
@@ -291,8 +297,12 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
                   (size_t)std::max<int64_t>(c->n[other], 1) * Dp);
   if (rc) return rc;
   float* tau = c->refl[other] + (size_t)Dp * Dp;
+  if (wide_dim(Dp)) {
+    rc = ensure(c, &c->tri_work, &c->cap_tri_work, wide_tridiag_work_floats(Dp));
+    if (rc) return rc;
+  }
   HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp, c->refl[other],
-                            tau, s));
+                            tau, s, c->tri_work));
   HIP_TRY(c, launch_form_q(c->refl[other], tau, Dp, c->q[other], s));
   HIP_TRY(c, launch_rot_gemm(X, nullptr, 0, c->n[other], c->q[other], 0, c->xrot[other], Dp, s));
   return FRECSYS_OK;
@@ -449,7 +459,7 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   const int Dp = padded_dim(cfg->dim);
   if (Dp == 0)
     return fail(nullptr, FRECSYS_ERR_UNSUPPORTED,
-                "dim " + std::to_string(cfg->dim) + " not supported (1..256 built)");
+                "dim " + std::to_string(cfg->dim) + " not supported (1..1024 built)");
   if (cfg->n_users < 0 || cfg->n_items < 0)
     return fail(nullptr, FRECSYS_ERR_INVALID, "negative entity counts");
   int cnt = 0;
@@ -492,6 +502,7 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H")) c->dual_max_h = atoi(v);
   if (const char* v = getenv("FRECSYS_DUAL_SERIAL")) c->dual_serial = atoi(v);
   if (const char* v = getenv("FRECSYS_SPLIT_ROWS")) c->split_rows = atoi(v);
+  if (const char* v = getenv("FRECSYS_WIDE_WS_MB")) c->wide_ws_mb = std::max(1, atoi(v));
   c->dual_max_h = std::min(c->dual_max_h, 32 * kDualMaxTiles);
   for (int s = 0; s < 2; ++s) {
     const size_t rows = (size_t)std::max<int64_t>(c->n[s], 1);
@@ -539,6 +550,8 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   for (int s = 0; s < 3; ++s)
     if (c->out_rot[s]) (void)hipFree(c->out_rot[s]);
   if (c->dual_table) (void)hipFree(c->dual_table);
+  if (c->tri_work) (void)hipFree(c->tri_work);
+  if (c->wide_ws) (void)hipFree(c->wide_ws);
   if (c->d_split) (void)hipFree(c->d_split);
   if (c->d_work) (void)hipFree(c->d_work);
   if (c->d_slabs) (void)hipFree(c->d_slabs);
@@ -764,6 +777,38 @@ int frecsys_set_gramian(frecsys_ctx* c, int32_t side, const float* host, int64_t
 }  // extern "C"
 
 namespace {
+// The d-space solve of the queue prefix ap.order[0..ap.n_rows): the tiled
+// one-workgroup-per-entity kernels (long histories split) up to Dp = 256,
+// the HBM-workspace batches of wide.hip at Dp = 512 / 1024.
+int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
+                  const std::function<int64_t(int64_t)>& heff, hipStream_t s,
+                  const std::string& pre, bool can_split) {
+  if (wide_dim(c->Dp)) {
+    const size_t slot = wide_slot_floats(c->Dp);
+    const int64_t budget = (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (slot * sizeof(float)));
+    const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(ap.n_rows, budget));
+    int rc = ensure(c, &c->wide_ws, &c->cap_wide_ws, (size_t)batch * slot);
+    if (rc) return rc;
+    const size_t k = ktimer_begin(c, pre + ".dspace", s);
+    HIP_TRY(c, launch_wide_solve(c->Dp, ap, c->wide_ws, batch, s));
+    ktimer_end(c, k, s);
+    return FRECSYS_OK;
+  }
+  if (can_split) {
+    int rc = plan_split(c, hs, ap.n_rows, heff, &ap);
+    if (rc) return rc;
+  }
+  if (ap.n_work > 0) {
+    const size_t k = ktimer_begin(c, pre + ".split", s);
+    HIP_TRY(c, launch_split_syrk(c->Dp, ap, s));
+    ktimer_end(c, k, s);
+  }
+  const size_t k = ktimer_begin(c, pre + ".dspace", s);
+  HIP_TRY(c, launch_solve(c->Dp, ap, s));
+  ktimer_end(c, k, s);
+  return FRECSYS_OK;
+}
+
 int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
                     bool force_dspace) {
   if (!c || !valid_side(side) || !p) return fail(c, FRECSYS_ERR_INVALID, "solve: bad arguments");
@@ -865,19 +910,9 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
     const std::string pre = names[side];
     ScopedTimer t(c, names[side]);
     if (!dual || n_dspace >= n_nonempty) {
-      SolveArgs ap = a;
-      if (c->Dp >= 32 && (int64_t)hs.size() == c->order_n[side]) {
-        rc = plan_split(c, hs, a.n_rows, heff, &ap);
-        if (rc) return rc;
-      }
-      if (ap.n_work > 0) {
-        const size_t k = ktimer_begin(c, pre + ".split", c->stream);
-        HIP_TRY(c, launch_split_syrk(c->Dp, ap, c->stream));
-        ktimer_end(c, k, c->stream);
-      }
-      const size_t k = ktimer_begin(c, pre + ".dspace", c->stream);
-      HIP_TRY(c, launch_solve(c->Dp, ap, c->stream));
-      ktimer_end(c, k, c->stream);
+      rc = launch_dspace(c, a, hs, heff, c->stream, pre,
+                         c->Dp >= 32 && (int64_t)hs.size() == c->order_n[side]);
+      if (rc) return rc;
     } else {
       // d-space solve of the long histories on stream2, concurrently with
       // the basis change + history-space solve of the rest on stream
@@ -894,16 +929,8 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
         SolveArgs ap = a;
         ap.n_rows = n_dspace;
-        rc = plan_split(c, hs, n_dspace, heff, &ap);
+        rc = launch_dspace(c, ap, hs, heff, s2, pre, true);
         if (rc) return rc;
-        if (ap.n_work > 0) {
-          const size_t k2 = ktimer_begin(c, pre + ".split", s2);
-          HIP_TRY(c, launch_split_syrk(c->Dp, ap, s2));
-          ktimer_end(c, k2, s2);
-        }
-        const size_t k2 = ktimer_begin(c, pre + ".dspace", s2);
-        HIP_TRY(c, launch_solve(c->Dp, ap, s2));
-        ktimer_end(c, k2, s2);
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
       }
       DualArgs d{};
@@ -1036,7 +1063,8 @@ int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, fl
     HIP_TRY(c, hipMemsetAsync(c->d_loss, 0, sizeof(float) * std::max<size_t>(rows, 1), c->stream));
   int64_t lo, hi;
   shard(c, side, &lo, &hi);
-  rc = ensure(c, &c->d_quad, &c->cap_quad, std::max<size_t>(rows, 1));
+  rc = ensure(c, &c->d_quad, &c->cap_quad,
+              std::max<size_t>(wide_dim(c->Dp) ? wide_quad_floats(c->Dp, hi - lo) : rows, 1));
   if (rc) return rc;
   LossArgs a{};
   a.quad = c->d_quad;

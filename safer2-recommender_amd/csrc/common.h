@@ -16,13 +16,13 @@ enum {
   KIND_CVAR_GRAD_V = 4,
 };
 
-__device__ __forceinline__ bool is_v_kind(int k) {
+__host__ __device__ __forceinline__ bool is_v_kind(int k) {
   return k == KIND_WEIGHTED_V || k == KIND_CVAR_GRAD_V;
 }
-__device__ __forceinline__ bool is_u_kind(int k) {
+__host__ __device__ __forceinline__ bool is_u_kind(int k) {
   return k == KIND_WEIGHTED_U || k == KIND_CVAR_GRAD_U;
 }
-__device__ __forceinline__ bool is_grad_kind(int k) {
+__host__ __device__ __forceinline__ bool is_grad_kind(int k) {
   return k == KIND_CVAR_GRAD_U || k == KIND_CVAR_GRAD_V;
 }
 

@@ -42,7 +42,7 @@ namespace frecsys_hip {
 
 namespace {
 
-constexpr int kMaxDp = 256;
+constexpr int kMaxDp = 1024;
 
 template <int TH>
 struct DualCfg {
@@ -58,19 +58,17 @@ struct DualCfg {
   static constexpr int NSTAGE = (TH <= 4) ? 1 : 2;  // LDS stages for the slab prefetch
   static constexpr int LOOP = ((NSTAGE * STG + ZS + 3) / 4) * 4;
   static constexpr int REGION0 = TILES > LOOP ? TILES : LOOP;
-  static constexpr int OFF_L = REGION0;             // l_k
-  static constexpr int OFF_DS = OFF_L + kMaxDp;     // D^-1/2
-  static constexpr int OFF_C = OFF_DS + kMaxDp;     // c_j
+  static constexpr int OFF_C = REGION0;             // c_j
   static constexpr int OFF_ID = OFF_C + HP;         // row ids
   static constexpr int OFF_B = OFF_ID + HP;         // s, then y
   static constexpr int OFF_X = OFF_B + HP;          // z
   static constexpr int PART = NTHR > NW * 32 ? NTHR : NW * 32;
   static constexpr int OFF_PART = OFF_X + HP;
   static constexpr int OFF_FLAG = OFF_PART + PART;
-  static constexpr int TOTAL = OFF_FLAG + 4;
-  static constexpr size_t BYTES = (size_t)TOTAL * 4;
+  static constexpr int OFF_L = OFF_FLAG + 4;        // l_k [Dp], then D^-1/2 [Dp]
   static constexpr int NQ = (HP * 8 + NTHR - 1) / NTHR;  // float4 per thread per slab
-  static_assert(BYTES <= 163840, "LDS budget");
+  static constexpr size_t bytes(int Dp) { return (size_t)(OFF_L + 2 * Dp) * 4; }
+  static_assert(bytes(kMaxDp) <= 163840, "LDS budget");
 };
 
 __device__ __forceinline__ int64_t virt_pos_d(int64_t k, int64_t h) {
@@ -154,7 +152,7 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
   float* stage = smem;
   float* zs = smem + C::NSTAGE * C::STG;
   float* lsub = smem + C::OFF_L;
-  float* dsq = smem + C::OFF_DS;
+  float* dsq = lsub + a.Dp;
   float* cvec = smem + C::OFF_C;
   int* ids = reinterpret_cast<int*>(smem + C::OFF_ID);
   float* bvec = smem + C::OFF_B;
@@ -356,10 +354,10 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs 
       *reinterpret_cast<float4*>(red + g * Dp + 4 * c4) = acc4;
     }
     lds_barrier();
-    if (tid < Dp) {
+    for (int i = tid; i < Dp; i += NTHR) {
       float v = 0.0f;
-      for (int gg = 0; gg < R; ++gg) v += red[gg * Dp + tid];
-      a.out_rot[blk_v(a.pos0 + blockIdx.x, tid, Dp)] = v;
+      for (int gg = 0; gg < R; ++gg) v += red[gg * Dp + i];
+      a.out_rot[blk_v(a.pos0 + blockIdx.x, i, Dp)] = v;
     }
   }
   mark(3);
@@ -454,10 +452,10 @@ struct WaveCfg {
   static constexpr int ZS = 32 * HP;
   static constexpr int REG = NT * 1024 > ZS ? NT * 1024 : ZS;
   static constexpr int OFF_ID = REG, OFF_C = OFF_ID + HP, OFF_B = OFF_C + HP, OFF_X = OFF_B + HP;
-  static constexpr int OFF_T = OFF_X + HP;   // l_k and D^-1/2 (table row), 2 * kMaxDp
-  static constexpr int OFF_FLAG = OFF_T + 2 * kMaxDp;
-  static constexpr int PW = OFF_FLAG + 4;  // floats per wave
-  static constexpr size_t BYTES = (size_t)4 * PW * 4;
+  static constexpr int OFF_FLAG = OFF_X + HP;
+  static constexpr int OFF_T = OFF_FLAG + 4;  // l_k and D^-1/2 (table row), 2 * Dp
+  static constexpr int pw(int Dp) { return OFF_T + 2 * Dp; }  // floats per wave
+  static constexpr size_t bytes(int Dp) { return (size_t)4 * pw(Dp) * 4; }
   static_assert(TH <= 2, "one history row per lane");
 };
 
@@ -471,7 +469,7 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   const int lo = lane & 31, hi = lane >> 5;
   const int64_t pos = (int64_t)blockIdx.x * 4 + wave;
   if (pos >= a.n_rows) return;  // whole wave; no workgroup barriers below
-  float* base = smem + wave * C::PW;
+  float* base = smem + wave * C::pw(a.Dp);
   float* zs = base;
   float* tiles = base;
   int* ids = reinterpret_cast<int*>(base + C::OFF_ID);
@@ -582,9 +580,11 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   wave_sync();
   chol_solve_wave<TH>(tiles, bvec, xvec, flag, lane, a.debug_skip);
 
-  // v = Y^T (c.*z): lane owns columns 4*lane .. 4*lane+3
+  // v = Y^T (c.*z): lane owns columns 4*lane + 256*cg .. +3
+  for (int cg = 0; 256 * cg < Dp; ++cg) {
+  const int c4 = 4 * lane + 256 * cg;
   float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (4 * lane < Dp && !(a.debug_skip & 64)) {
+  if (c4 < Dp && !(a.debug_skip & 64)) {
     for (int j0 = 0; j0 < ntot; j0 += 8) {
       float4 rv[8];
       float wv[8];
@@ -595,7 +595,7 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
         rv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (jj < ntot) {
           wv[u] = cvec[jj] * xvec[jj];
-          rv[u] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)ids[jj] * Dp + 4 * lane);
+          rv[u] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)ids[jj] * Dp + c4);
         }
       }
 #pragma unroll
@@ -607,12 +607,13 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
       }
     }
   }
-  if (4 * lane < Dp) {
+  if (c4 < Dp) {
     const int64_t pp = a.pos0 + pos;
-    a.out_rot[blk_v(pp, 4 * lane + 0, Dp)] = v4.x;
-    a.out_rot[blk_v(pp, 4 * lane + 1, Dp)] = v4.y;
-    a.out_rot[blk_v(pp, 4 * lane + 2, Dp)] = v4.z;
-    a.out_rot[blk_v(pp, 4 * lane + 3, Dp)] = v4.w;
+    a.out_rot[blk_v(pp, c4 + 0, Dp)] = v4.x;
+    a.out_rot[blk_v(pp, c4 + 1, Dp)] = v4.y;
+    a.out_rot[blk_v(pp, c4 + 2, Dp)] = v4.z;
+    a.out_rot[blk_v(pp, c4 + 3, Dp)] = v4.w;
+  }
   }
   if (lane == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
@@ -621,7 +622,7 @@ template <int TH>
 hipError_t launch_wave_t(const DualArgs& a, hipStream_t s) {
   using C = WaveCfg<TH>;
   const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
-  hipLaunchKernelGGL(dual_wave_kernel<TH>, dim3(nb), dim3(256), C::BYTES, s, a);
+  hipLaunchKernelGGL(dual_wave_kernel<TH>, dim3(nb), dim3(256), C::bytes(a.Dp), s, a);
   return hipGetLastError();
 }
 
@@ -632,12 +633,12 @@ hipError_t launch_dual_t(const DualArgs& a, hipStream_t s) {
   if (!attr) {
     hipError_t err = hipFuncSetAttribute((const void*)dual_solve_kernel<TH>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)C::BYTES);
+                                         (int)C::bytes(kMaxDp));
     if (err != hipSuccess) return err;
     attr = true;
   }
-  hipLaunchKernelGGL(dual_solve_kernel<TH>, dim3((unsigned)a.n_rows), dim3(C::NTHR), C::BYTES, s,
-                     a);
+  hipLaunchKernelGGL(dual_solve_kernel<TH>, dim3((unsigned)a.n_rows), dim3(C::NTHR),
+                     C::bytes(a.Dp), s, a);
   return hipGetLastError();
 }
 

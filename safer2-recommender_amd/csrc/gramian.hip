@@ -207,13 +207,14 @@ int64_t gram_num_blocks(int Dp, int64_t n) {
 }
 
 size_t gram_workspace_floats(int Dp, int64_t n) {
-  const int64_t nblk = gram_num_blocks(Dp, n);
+  const int64_t nblk = wide_dim(Dp) ? wide_gram_num_blocks(n) : gram_num_blocks(Dp, n);
   if (Dp <= 16) return (size_t)(nblk > 0 ? nblk : 1) * Dp * Dp;
   const int T = Dp / 32;
   return (size_t)(nblk > 0 ? nblk : 1) * (T * (T + 1) / 2) * 1024;
 }
 
 hipError_t launch_gramian(int Dp, const GramArgs& a, hipStream_t s) {
+  if (wide_dim(Dp)) return launch_wide_gramian(Dp, a, s);
   switch (Dp) {
     case 8: return launch_small<8>(a, s);
     case 16: return launch_small<16>(a, s);

@@ -136,7 +136,7 @@ hipError_t launch_dual(int tiles, const DualArgs& a, hipStream_t s);
 // (one workgroup): T's diagonal / subdiagonal, the reflectors (row k of Vh,
 // entries k+1..Dp-1) and their tau.
 hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
-                          float* tau, hipStream_t s);
+                          float* tau, hipStream_t s, float* work = nullptr);
 // Q = H_0 H_1 ... H_{Dp-3} from the reflectors, row-major Dp x Dp.
 hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s);
 // Y[row] = X[row] * (trans ? Q^T : Q) for rows r0..r0+n-1, or for the
@@ -154,11 +154,31 @@ __host__ __device__ inline int64_t blk_t(int64_t p, int j, int k, int Dp) {
   return ((p >> 6) * 3 * Dp + j * Dp + k) * 64 + (p & 63);
 }
 hipError_t launch_gramian(int Dp, const GramArgs& a, hipStream_t s);
+
+// Wide dims, Dp = 512 / 1024 (wide.hip).  d-space solve with A in an HBM
+// workspace ([batch][wide_slot_floats(Dp)]), entities a.order[0..n_rows)
+// in batches; Gramian by 128x128 block pairs; per-step tridiagonalisation
+// (work: wide_tridiag_work_floats); rotations; user loss (a.quad holds
+// wide_quad_floats partials).
+bool wide_dim(int Dp);
+size_t wide_slot_floats(int Dp);
+int64_t wide_gram_num_blocks(int64_t n);
+hipError_t launch_wide_gramian(int Dp, const GramArgs& g, hipStream_t s);
+hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batch,
+                             hipStream_t s);
+size_t wide_tridiag_work_floats(int Dp);
+hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
+                               float* tau, float* work, hipStream_t s);
+hipError_t launch_wide_rot(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
+                           const float* Q, int trans, float* Y, int Dp, hipStream_t s,
+                           int x_blocked);
+size_t wide_quad_floats(int Dp, int64_t rows);
+hipError_t launch_wide_user_loss(int Dp, const LossArgs& a, hipStream_t s);
 hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s);
 hipError_t launch_zero_gram(int Dp, float* G, hipStream_t s);
 
-// Padded leading dimension for a logical dimension (8, 16, then multiples
-// of 32 up to 256).  Returns 0 when unsupported.
+// Padded leading dimension for a logical dimension (8, 16, multiples of 32
+// up to 256, then 512 and 1024).  Returns 0 when unsupported.
 int padded_dim(int dim);
 
 }  // namespace frecsys_hip

@@ -225,6 +225,7 @@ hipError_t launch(const LossArgs& a, hipStream_t s) {
 
 hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
+  if (wide_dim(Dp)) return launch_wide_user_loss(Dp, a, s);
   switch (Dp) {
     case 8: return launch<8>(a, s);
     case 16: return launch<16>(a, s);

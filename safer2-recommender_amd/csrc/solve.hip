@@ -521,6 +521,8 @@ int padded_dim(int dim) {
   if (dim <= 8) return 8;
   if (dim <= 16) return 16;
   if (dim <= 256) return ((dim + 31) / 32) * 32;
+  if (dim <= 512) return 512;
+  if (dim <= 1024) return 1024;
   return 0;
 }
 

@@ -199,39 +199,41 @@ __global__ void __launch_bounds__(1024)
 
 // One wave per column c of Q: q = H_0 (H_1 (... H_{n-3} e_c)); H_k leaves
 // columns c <= k alone, so the product starts at k = min(c-1, n-3).
+// RPL = rows per lane (n <= 64 * RPL).
+template <int RPL>
 __global__ void __launch_bounds__(256)
     form_q_kernel(const float* __restrict__ Vh, const float* __restrict__ tau, int n, float* Q) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (c >= n) return;  // no barriers below
-  float q[4];
+  float q[RPL];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) q[r] = (lane + 64 * r == c) ? 1.0f : 0.0f;
+  for (int r = 0; r < RPL; ++r) q[r] = (lane + 64 * r == c) ? 1.0f : 0.0f;
   int k = c - 1 < n - 3 ? c - 1 : n - 3;
-  float vn[4];
+  float vn[RPL];
   auto load = [&](int kk, float* dst) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < RPL; ++r) {
       const int row = lane + 64 * r;
       dst[r] = (kk >= 0 && row > kk && row < n) ? Vh[(int64_t)kk * n + row] : 0.0f;
     }
   };
   load(k, vn);
   for (; k >= 0; --k) {
-    float vk[4];
+    float vk[RPL];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) vk[r] = vn[r];
+    for (int r = 0; r < RPL; ++r) vk[r] = vn[r];
     const float t = tau[k];
     load(k - 1, vn);  // prefetch the next reflector under this one's reduction
     if (t == 0.0f) continue;
     float d = 0.0f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) d += vk[r] * q[r];
+    for (int r = 0; r < RPL; ++r) d += vk[r] * q[r];
     d = wave_sum(d) * t;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) q[r] -= d * vk[r];
+    for (int r = 0; r < RPL; ++r) q[r] -= d * vk[r];
   }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < RPL; ++r) {
     const int row = lane + 64 * r;
     if (row < n) Q[(int64_t)row * n + c] = q[r];
   }
@@ -332,16 +334,22 @@ hipError_t launch_rot(const float* X, const QueueRec* rows, int64_t r0, int64_t 
 }  // namespace
 
 hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
-                          float* tau, hipStream_t s) {
+                          float* tau, hipStream_t s, float* work) {
+  if (wide_dim(Dp)) return launch_wide_tridiag(G, Dp, tdiag, toff, Vh, tau, work, s);
   if (Dp < 4 || Dp > 256) return hipErrorInvalidValue;
   hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(1024), 0, s, G, Dp, tdiag, toff, Vh, tau);
   return hipGetLastError();
 }
 
 hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s) {
-  if (Dp < 4 || Dp > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(form_q_kernel, dim3((unsigned)((Dp + 3) / 4)), dim3(256), 0, s, Vh, tau, Dp,
-                     Q);
+  if (Dp < 4 || Dp > 1024) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)((Dp + 3) / 4));
+  if (Dp <= 256)
+    hipLaunchKernelGGL(form_q_kernel<4>, grid, dim3(256), 0, s, Vh, tau, Dp, Q);
+  else if (Dp <= 512)
+    hipLaunchKernelGGL(form_q_kernel<8>, grid, dim3(256), 0, s, Vh, tau, Dp, Q);
+  else
+    hipLaunchKernelGGL(form_q_kernel<16>, grid, dim3(256), 0, s, Vh, tau, Dp, Q);
   return hipGetLastError();
 }
 
@@ -349,6 +357,7 @@ hipError_t launch_rot_gemm(const float* X, const QueueRec* rows, int64_t r0, int
                            const float* Q, int trans, float* Y, int Dp, hipStream_t s,
                            int x_blocked) {
   if (n <= 0) return hipSuccess;
+  if (wide_dim(Dp)) return launch_wide_rot(X, rows, r0, n, Q, trans, Y, Dp, s, x_blocked);
   switch (Dp) {
     case 64: return launch_rot<2>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
     case 96: return launch_rot<3>(X, rows, r0, n, Q, trans, Y, s, x_blocked);

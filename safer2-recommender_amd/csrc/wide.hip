@@ -1,0 +1,828 @@
+// wide.hip -- the solve loop at d = 512 / 1024 (Dp > 256) on gfx950.
+//
+// At these widths a d x d normal matrix no longer fits one CU (1 MB / 4 MB
+// fp32 against 160 KB of LDS), so the d-space solve of the reference's
+// Project / ProjectU / ProjectV (ials.h:88-144, safer2.h:104-221,
+// erm_mf.h:91-210, cvar_mf.h:182-229) is split across kernels with A in an
+// HBM workspace, a bounded batch of entities at a time:
+//
+//   wide_syrk_kernel<1>  grid (entity, 128x128 block pair of A's lower
+//                        triangle): the pair's 16 32x32 tiles accumulate
+//                        X_h^T D X_h over the gathered history rows with
+//                        v_mfma_f32_32x32x2_f32 (rows staged through LDS, 16
+//                        per chunk, one chunk ahead; row ids two chunks
+//                        ahead), starting from the G part of A; the diagonal
+//                        pairs also form their 128 entries of b.
+//   wide_chol_kernel     one workgroup (8 waves) per entity: right-looking
+//                        blocked Cholesky over the workspace tiles -- the
+//                        diagonal tile factored and inverted in LDS
+//                        (diag_factor_inv), the panel column TRSM'd by MFMA
+//                        into LDS (it is read by every trailing update of the
+//                        step), trailing tiles updated in place, y = L^-1 b
+//                        riding along, then x = L^-T y.
+//   wide_grad_kernel     CVaR-MF's gradient step with the stale upper
+//                        triangle (cvar_mf.h:133, 179).
+//
+// Most entities never come here: the history-space path (dual.hip) takes
+// every h_eff <= 256 at any width.  Its basis at these widths:
+//   tridiag_step_kernel  one launch per Householder step (no grid barrier):
+//                        each workgroup finishes the previous step's rank-2
+//                        update on its 16 columns (ping-pong copy of the
+//                        matrix), re-forms the step's reflector from the
+//                        updated row k itself, and writes its columns of
+//                        p = tau A v for the next launch.
+//   rot_wide_kernel      Y = X Q / X Q^T, 64 rows x 128 columns per
+//                        workgroup, K streamed in 32-wide slabs; also the
+//                        u^T G u partials of the user loss.
+// and the Gramian: wide_syrk_kernel<0> (split-K over row blocks x block
+// pairs) + wide_gram_reduce_kernel (fixed order, deterministic).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "chol.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace frecsys_hip {
+
+namespace {
+
+constexpr int WB = 128;    // block-pair edge
+constexpr int WR = 16;     // rows per staged chunk
+constexpr int WRING = 4;   // row-id ring slots
+constexpr int kWideMaxBlocks = 64;
+
+__device__ __forceinline__ void pair_of(int pidx, int& BI, int& BJ) {
+  BI = 0;
+  while ((BI + 1) * (BI + 2) / 2 <= pidx) ++BI;
+  BJ = pidx - BI * (BI + 1) / 2;
+}
+
+__device__ __forceinline__ int64_t wide_virt_pos(int64_t k, int64_t h) {
+  return k < h ? k : (h - 128 + (k - h));
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int tid = threadIdx.x, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  float s = 0.0f;
+  for (int w = 0; w < nw; ++w) s += red[w];
+  return s;
+}
+
+// MODE 0: partial Gramian of rows [r0, r1) (operand weight g.w);
+// MODE 1: assembly of entity order[pos0 + blockIdx.x] into its workspace slot.
+template <int MODE>
+__global__ void __launch_bounds__(256)
+    wide_syrk_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws) {
+  __shared__ __attribute__((aligned(16))) float xa[2][WR * WB];
+  __shared__ __attribute__((aligned(16))) float xb[2][WR * WB];
+  __shared__ int ring_id[WRING * WR];
+  __shared__ float ring_sa[WRING * WR], ring_bw[WRING * WR];
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int BI, BJ;
+  pair_of(blockIdx.y, BI, BJ);
+  const bool dgp = BI == BJ;
+  const int T = Dp >> 5, NT = T * (T + 1) / 2;
+  const int kind = a.kind;
+  const bool vk = MODE == 1 && is_v_kind(kind);
+
+  int64_t r0 = 0, nrow = 0, e = 0, h = 0, p0 = 0;
+  if (MODE == 0) {
+    r0 = g.row0 + (int64_t)blockIdx.x * rpb;
+    int64_t r1 = r0 + rpb;
+    if (r1 > g.row0 + g.n) r1 = g.row0 + g.n;
+    nrow = r1 > r0 ? r1 - r0 : 0;
+  } else {
+    const QueueRec rec = a.order[pos0 + blockIdx.x];
+    e = rec.entity;
+    h = rec.h;
+    p0 = rec.p0;
+    if (h == 0) return;  // untouched entity (no workgroup barrier passed yet)
+    int64_t extra = 0;
+    if (vk && a.quirk && h > 128 && (h % 128) != 0) extra = 128 - (h % 128);
+    nrow = h + extra;
+  }
+  const int nchunks = (int)((nrow + WR - 1) / WR);
+
+  auto ring_load = [&](int c, int& id, float& sa, float& bw) {
+    const int64_t k = (int64_t)c * WR + tid;
+    id = -1;
+    sa = 0.0f;
+    bw = 0.0f;
+    if (k < nrow) {
+      if (MODE == 0) {
+        id = (int)(r0 + k);
+        sa = 1.0f;
+        bw = g.w ? g.w[r0 + k] : 1.0f;  // weight of the B operand
+      } else {
+        id = a.col[p0 + wide_virt_pos(k, h)];
+        if (vk) {  // rows pre-scaled by sqrt(nu); rhs weight nu / sqrt(nu) (safer2.h:190-192)
+          const float nu = a.other_weight[id];
+          sa = sqrtf(nu);
+          bw = (k < h && sa > 0.0f) ? nu / sa : 0.0f;
+        } else {
+          sa = 1.0f;
+          bw = 1.0f;
+        }
+      }
+    }
+  };
+  auto ring_store = [&](int c, int id, float sa, float bw) {
+    const int s = (c % WRING) * WR + tid;
+    ring_id[s] = id;
+    ring_sa[s] = sa;
+    ring_bw[s] = bw;
+  };
+  const float* X = MODE == 0 ? g.X : a.X;
+  float4 regs[4];
+  auto load_data = [&](int c) {
+    const int slot = c % WRING;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int sidx = tid + 256 * q;
+      const int r = sidx >> 6, f = sidx & 63;
+      regs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!(dgp && f >= 32)) {
+        const int col = f < 32 ? WB * BI + 4 * f : WB * BJ + 4 * (f - 32);
+        const int id = ring_id[slot * WR + r];
+        if (id >= 0) regs[q] = *reinterpret_cast<const float4*>(X + (int64_t)id * Dp + col);
+      }
+    }
+  };
+  auto store_stage = [&](int buf, int c) {
+    const int slot = c % WRING;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int sidx = tid + 256 * q;
+      const int r = sidx >> 6, f = sidx & 63;
+      if (dgp && f >= 32) continue;
+      float4 v = regs[q];
+      const float sa = ring_sa[slot * WR + r];
+      if (MODE == 1 && vk) {
+        v.x *= sa;
+        v.y *= sa;
+        v.z *= sa;
+        v.w *= sa;
+      }
+      float4 vb = v;
+      if (MODE == 0) {  // B operand carries the row weight
+        const float bw = ring_bw[slot * WR + r];
+        vb.x *= bw;
+        vb.y *= bw;
+        vb.z *= bw;
+        vb.w *= bw;
+      }
+      if (f < 32) {
+        *reinterpret_cast<float4*>(&xa[buf][r * WB + 4 * f]) = v;
+        if (dgp) *reinterpret_cast<float4*>(&xb[buf][r * WB + 4 * f]) = vb;
+      } else {
+        *reinterpret_cast<float4*>(&xb[buf][r * WB + 4 * (f - 32)]) = vb;
+      }
+    }
+  };
+
+  if (tid < WR && nchunks > 0) {
+    int id;
+    float sa, bw;
+    ring_load(0, id, sa, bw);
+    ring_store(0, id, sa, bw);
+    if (nchunks > 1) {
+      ring_load(1, id, sa, bw);
+      ring_store(1, id, sa, bw);
+    }
+  }
+
+  // accumulators start from the G part of A (MODE 1, as solve.hip):
+  //  iALS w*G + lam*I, U h*w*G, V w*G, CVaR 0
+  const float hf = (float)h;
+  float omega = 1.0f, lam = 0.0f;
+  const bool grad = MODE == 1 && is_grad_kind(kind);
+  if (MODE == 1) {
+    omega = (is_u_kind(kind) && a.entity_weight) ? a.entity_weight[e] : 1.0f;
+    lam = entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other, a.entity_reg, e,
+                        a.lambda_is_reg);
+  }
+  const float gscale = kind == KIND_IALS ? a.w : (is_u_kind(kind) ? hf * a.w : a.w);
+  f32x16 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    acc[j] = f32x16{0.f};
+    if (MODE == 1 && !grad && (!dgp || j <= wave)) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int gi = WB * BI + 32 * wave + acc_row(q, hi), gj = WB * BJ + 32 * j + lo;
+        float v = gscale * a.G[(int64_t)gi * Dp + gj];
+        if (kind == KIND_IALS && gi == gj) v += lam;
+        acc[j][q] = v;
+      }
+    }
+  }
+  float bacc = 0.0f;
+  lds_barrier();
+  if (nchunks > 0) {
+    load_data(0);
+    store_stage(0, 0);
+  }
+  lds_barrier();
+
+  for (int c = 0; c < nchunks; ++c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nchunks;
+    const bool ring_more = (tid < WR) && (c + 2 < nchunks);
+    if (more) load_data(c + 1);
+    int nid = -1;
+    float nsa = 0.f, nbw = 0.f;
+    if (ring_more) ring_load(c + 2, nid, nsa, nbw);
+    const float* sa_ = xa[buf];
+    const float* sb_ = xb[buf];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!dgp || j <= wave) {  // wave-uniform
+#pragma unroll
+        for (int s = 0; s < WR / 2; ++s) {
+          const int row = 2 * s + hi;
+          acc[j] = mfma32(sa_[row * WB + 32 * wave + lo], sb_[row * WB + 32 * j + lo], acc[j]);
+        }
+      }
+    }
+    if (MODE == 1 && dgp && tid < WB) {
+      const int slot = c % WRING;
+#pragma unroll 4
+      for (int r = 0; r < WR; ++r) bacc += ring_bw[slot * WR + r] * sa_[r * WB + tid];
+    }
+    if (more) store_stage(buf ^ 1, c + 1);
+    if (ring_more) ring_store(c + 2, nid, nsa, nbw);
+    lds_barrier();
+  }
+
+  if (MODE == 0) {
+    float* P = g.partials + (int64_t)blockIdx.x * NT * 1024;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!dgp || j <= wave) {
+        const int I = 4 * BI + wave, J = 4 * BJ + j;
+        float* tile = P + (int64_t)tidx(I, J) * 1024;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) tile[acc_row(q, hi) * 32 + lo] = acc[j][q];
+      }
+    }
+    return;
+  }
+
+  // epilogue: finish A (per kind, as solve.hip) into the workspace tiles
+  float* slot = ws + (int64_t)blockIdx.x * ((int64_t)NT * 1024 + Dp);
+  const float us = omega / hf;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!dgp || j <= wave) {
+      const int I = 4 * BI + wave, J = 4 * BJ + j;
+      float* tile = slot + (int64_t)tidx(I, J) * 1024;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = acc_row(q, hi);
+        const int gi = 32 * I + i, gj = 32 * J + lo;
+        const bool dg = gi == gj;
+        float v = acc[j][q];
+        if (grad) v = assemble(kind, v, a.G[(int64_t)gi * Dp + gj], dg, a.w, lam, hf, omega);
+        else if (is_u_kind(kind)) v = v * us + (dg ? lam : 0.0f);
+        else if (vk) v = v + (dg ? lam : 0.0f);
+        tile[i * 32 + lo] = v;
+      }
+    }
+  }
+  if (dgp && tid < WB) {
+    float b = bacc;
+    if (is_u_kind(kind)) b *= us;  // rhs *= weight / history_size
+    slot[(int64_t)NT * 1024 + WB * BI + tid] = b;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    wide_gram_reduce_kernel(const float* __restrict__ P, int64_t nblk, float* __restrict__ G,
+                            int Dp) {
+  const int64_t el = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (el >= (int64_t)Dp * Dp) return;
+  const int gi = (int)(el / Dp), gj = (int)(el % Dp);
+  if (gi < gj) return;
+  const int T = Dp >> 5, NT = T * (T + 1) / 2;
+  const int64_t off = (int64_t)tidx(gi >> 5, gj >> 5) * 1024 + (gi & 31) * 32 + (gj & 31);
+  float s = 0.0f;
+  for (int64_t b = 0; b < nblk; ++b) s += P[b * NT * 1024 + off];
+  G[(int64_t)gi * Dp + gj] = s;
+  G[(int64_t)gj * Dp + gi] = s;
+}
+
+// One workgroup (8 waves) per entity of the batch: A x = b with A's lower
+// tiles in the entity's workspace slot (row-major 32x32 tiles, tidx order).
+// LDS: the diagonal slot, the panel column (swizzled), b / y, x, partials.
+__global__ void __launch_bounds__(512)
+    wide_chol_kernel(SolveArgs a, int Dp, int64_t pos0, float* ws) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NW = 8;
+  const int T = Dp >> 5, NT = T * (T + 1) / 2;
+  float* dslot = smem;
+  float* pan = smem + 1024;
+  float* bvec = pan + T * 1024;
+  float* xvec = bvec + Dp;
+  float* part = xvec + Dp;
+  float* ytmp = part + NW * 32;
+  int* flag = reinterpret_cast<int*>(ytmp + 32);
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const QueueRec rec = a.order[pos0 + blockIdx.x];
+  const int64_t e = rec.entity;
+  if (rec.h == 0) return;
+  float* slot = ws + (int64_t)blockIdx.x * ((int64_t)NT * 1024 + Dp);
+  auto gtile = [&](int I, int J) { return slot + (int64_t)tidx(I, J) * 1024; };
+  for (int i = tid; i < Dp; i += 512) bvec[i] = slot[(int64_t)NT * 1024 + i];
+  if (tid == 0) flag[0] = 0;
+  __syncthreads();
+
+#pragma unroll 1
+  for (int p = 0; p < T; ++p) {
+    // diagonal tile: L_pp^-1 into dslot (and back to the workspace for the
+    // back substitution), y_p = L_pp^-1 b_p
+    if (wave == 0) {
+      const float* A = gtile(p, p);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int idx = lane + 64 * i;
+        dslot[sw(idx >> 5, idx & 31)] = A[idx];
+      }
+      wave_lds_sync();
+      if (!diag_factor_inv(dslot, lane) && lane == 0) flag[0] = 1;
+      wave_lds_sync();
+      float y = 0.0f;
+#pragma unroll 8
+      for (int k = 0; k < 32; ++k) y += dslot[sw(lo, k)] * bvec[32 * p + k];
+      wave_lds_sync();
+      if (hi == 0) bvec[32 * p + lo] = y;
+      float* Aw = gtile(p, p);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int idx = lane + 64 * i;
+        Aw[idx] = dslot[sw(idx >> 5, idx & 31)];
+      }
+    }
+    __syncthreads();
+    // panel: L_Ip = A_Ip (L_pp^-1)^T into LDS (and the workspace); b_I -= L_Ip y_p
+#pragma unroll 1
+    for (int I = p + 1 + wave; I < T; I += NW) {
+      float* Pl = pan + I * 1024;
+      float* Ag = gtile(I, p);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int idx = lane + 64 * i;
+        Pl[sw(idx >> 5, idx & 31)] = Ag[idx];
+      }
+      wave_lds_sync();
+      const f32x16 u = tile_pqT(Pl, dslot, lo, hi);
+      wave_lds_sync();
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int r = acc_row(q, hi);
+        Pl[sw(r, lo)] = u[q];
+        Ag[r * 32 + lo] = u[q];
+      }
+      wave_lds_sync();
+      if (hi == 0) {
+        float s = 0.0f;
+#pragma unroll 8
+        for (int k = 0; k < 32; ++k) s += Pl[sw(lo, k)] * bvec[32 * p + k];
+        bvec[32 * I + lo] -= s;
+      }
+    }
+    __syncthreads();
+    // trailing update A_IJ -= L_Ip L_Jp^T, p < J <= I
+    const int m = T - 1 - p, ntr = m * (m + 1) / 2;
+#pragma unroll 1
+    for (int tt = wave; tt < ntr; tt += NW) {
+      int Ir = 0;
+      while ((Ir + 1) * (Ir + 2) / 2 <= tt) ++Ir;
+      const int Jr = tt - Ir * (Ir + 1) / 2;
+      const int I = p + 1 + Ir, J = p + 1 + Jr;
+      float* Ag = gtile(I, J);
+      f32x16 v;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = Ag[acc_row(q, hi) * 32 + lo];
+      const f32x16 u = tile_pqT(pan + I * 1024, pan + J * 1024, lo, hi);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) Ag[acc_row(q, hi) * 32 + lo] = v[q] - u[q];
+    }
+    __syncthreads();
+  }
+
+  // back substitution x_p = L_pp^-T (y_p - sum_{q>p} L_qp^T x_q)
+#pragma unroll 1
+  for (int p = T - 1; p >= 0; --p) {
+    float pr = 0.0f;
+    for (int q = p + 1 + wave; q < T; q += NW) {
+      const float* L = gtile(q, p);
+#pragma unroll 4
+      for (int mm = 16 * hi; mm < 16 * hi + 16; ++mm) pr += L[mm * 32 + lo] * xvec[32 * q + mm];
+    }
+    pr += __shfl_xor(pr, 32);
+    if (hi == 0) part[wave * 32 + lo] = pr;
+    __syncthreads();
+    if (wave == 0) {
+      float r = bvec[32 * p + lo];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) r -= part[w * 32 + lo];
+      const float* Li = gtile(p, p);
+      float x = 0.0f;
+#pragma unroll 8
+      for (int i = 0; i < 32; ++i) x += Li[i * 32 + lo] * rdlane(r, i);
+      if (hi == 0) xvec[32 * p + lo] = x;
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < Dp; i += 512) a.out[e * Dp + i] = xvec[i];
+  if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
+}
+
+// CVaR-MF: x = e - eta (A_full e - b), A_full's strict upper part the stale
+// G part (cvar_upper); one workgroup per entity.
+__global__ void __launch_bounds__(256)
+    wide_grad_kernel(SolveArgs a, int Dp, int64_t pos0, float* ws) {
+  __shared__ float ev[1024];
+  const int T = Dp >> 5, NT = T * (T + 1) / 2;
+  const QueueRec rec = a.order[pos0 + blockIdx.x];
+  const int64_t e = rec.entity;
+  if (rec.h == 0) return;
+  const float* slot = ws + (int64_t)blockIdx.x * ((int64_t)NT * 1024 + Dp);
+  const int kind = a.kind;
+  const float omega = (is_u_kind(kind) && a.entity_weight) ? a.entity_weight[e] : 1.0f;
+  for (int i = threadIdx.x; i < Dp; i += 256) ev[i] = a.E[e * Dp + i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < Dp; i += 256) {
+    float y = 0.0f;
+    for (int j = 0; j < Dp; ++j) {
+      float aij;
+      if (j <= i)
+        aij = slot[(int64_t)tidx(i >> 5, j >> 5) * 1024 + (i & 31) * 32 + (j & 31)];
+      else
+        aij = cvar_upper(kind, a.G[(int64_t)i * Dp + j], a.w, omega);
+      y += aij * ev[j];
+    }
+    a.out[e * Dp + i] = ev[i] - a.eta * (y - slot[(int64_t)NT * 1024 + i]);
+  }
+}
+
+// One Householder step k of G = Q T Q^T (LAPACK sytd2, lower; v(k+1) = 1).
+// Ain holds the matrix after step k-1's reflection EXCEPT its rank-2
+// update, which this launch applies: rows / columns >= k of
+// A - v w^T - w v^T with v = reflector k-1 (Vh row k-1, tau[k-1]) and
+// w = p + K v, K = -tau/2 p.v, p = pin (written by launch k-1).  Every
+// workgroup re-forms row k of the updated matrix and reflector k from it;
+// workgroup b then updates columns [16b, 16b+16) into Aout (rows >= k+1)
+// and writes those columns of p_k = tau_k A v_k to pout.
+__global__ void __launch_bounds__(256)
+    tridiag_step_kernel(const float* __restrict__ Ain, float* __restrict__ Aout, int n, int k,
+                        const float* __restrict__ pin, float* __restrict__ pout,
+                        float* __restrict__ Vh, float* __restrict__ tau,
+                        float* __restrict__ tdiag, float* __restrict__ toff) {
+  constexpr int CW = 16;
+  const int c0 = blockIdx.x * CW;
+  if (blockIdx.x != 0 && c0 + CW <= k + 1) return;  // whole workgroup, before any barrier
+  __shared__ float vp[1024], wv[1024], vk[1024];
+  __shared__ float red[8];
+  __shared__ float pc[16][CW + 1];
+  const int tid = threadIdx.x;
+  // previous reflector and w
+  const float tp = k > 0 ? tau[k - 1] : 0.0f;
+  for (int r = tid; r < n; r += 256) {
+    float v = 0.0f;
+    if (k > 0 && tp != 0.0f) v = r == k ? 1.0f : (r > k ? Vh[(int64_t)(k - 1) * n + r] : 0.0f);
+    vp[r] = v;
+  }
+  __syncthreads();
+  float d = 0.0f;
+  if (tp != 0.0f)
+    for (int r = k + tid; r < n; r += 256) d += pin[r] * vp[r];
+  d = block_sum(d, red);
+  const float K = -0.5f * tp * d;
+  for (int r = tid; r < n; r += 256) wv[r] = (tp != 0.0f && r >= k) ? pin[r] + K * vp[r] : 0.0f;
+  __syncthreads();
+  // row k of the updated matrix -> reflector k
+  const float vpk = vp[k], wk = wv[k];
+  float xn = 0.0f;
+  for (int r = k + tid; r < n; r += 256) {
+    const float ck = Ain[(int64_t)k * n + r] - vpk * wv[r] - wk * vp[r];
+    vk[r] = ck;
+    if (r >= k + 2) xn += ck * ck;
+  }
+  xn = block_sum(xn, red);  // (barriers inside: vk complete)
+  const float dkk = vk[k];
+  float beta = 0.0f, tk = 0.0f, scal = 0.0f;
+  if (k + 1 < n) {
+    const float alpha = vk[k + 1];
+    if (xn == 0.0f) {
+      beta = alpha;
+      tk = 0.0f;
+    } else {
+      beta = -copysignf(sqrtf(alpha * alpha + xn), alpha);
+      tk = (beta - alpha) / beta;
+      scal = 1.0f / (alpha - beta);
+    }
+  }
+  __syncthreads();
+  for (int r = tid; r < n; r += 256) {
+    float v = 0.0f;
+    if (r == k + 1) v = 1.0f;
+    else if (r >= k + 2) v = tk != 0.0f ? vk[r] * scal : 0.0f;
+    vk[r] = v;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    if (tid == 0) {
+      tdiag[k] = dkk;
+      toff[k] = k + 1 < n ? beta : 0.0f;
+      tau[k] = tk;
+    }
+    if (k + 1 < n)
+      for (int r = k + 1 + tid; r < n; r += 256) Vh[(int64_t)k * n + r] = vk[r];
+  }
+  if (k + 1 >= n) return;
+  // my columns: finish step k-1's update (rows >= k+1) and p_k
+  const int c = c0 + (tid & (CW - 1)), rg = tid >> 4;
+  float pacc = 0.0f;
+  if (c >= k + 1 && c < n) {
+    const float vpc = vp[c], wc = wv[c];
+    for (int r = k + 1 + rg; r < n; r += 16) {
+      const float v = Ain[(int64_t)r * n + c] - vp[r] * wc - wv[r] * vpc;
+      Aout[(int64_t)r * n + c] = v;
+      pacc += v * vk[r];
+    }
+  }
+  pc[rg][tid & (CW - 1)] = pacc;
+  __syncthreads();
+  if (tid < CW) {
+    const int cc = c0 + tid;
+    float s = 0.0f;
+#pragma unroll
+    for (int g2 = 0; g2 < 16; ++g2) s += pc[g2][tid];
+    if (cc >= k + 1 && cc < n) pout[cc] = tk * s;
+  }
+}
+
+// Y = X B (B = Q, or Q^T with trans) for 64 rows x 128 columns per
+// workgroup; with qpart, instead the partial row dots sum_c (X G)[r][c] X[r][c]
+// over the block's columns (u^T G u, summed over blocks by the loss).
+__global__ void __launch_bounds__(256)
+    rot_wide_kernel(const float* __restrict__ X, const QueueRec* __restrict__ rows, int64_t r0,
+                    int64_t n, const float* __restrict__ Q, int trans, float* __restrict__ Y,
+                    int x_blocked, int Dp, float* __restrict__ qpart) {
+  __shared__ float xs[64 * 33];
+  __shared__ float bs[32 * (WB + 1)];
+  __shared__ int64_t rid[64];
+  __shared__ float qred[2][64];
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t base = (int64_t)blockIdx.x * 64;
+  const int cb = blockIdx.y;
+  if (tid < 64) {
+    const int64_t r = base + tid;
+    rid[tid] = r < n ? (rows ? (int64_t)rows[r].entity : r0 + r) : -1;
+  }
+  __syncthreads();
+  const int R = wave & 1, Cs = (wave >> 1) * 2;
+  f32x16 acc[2] = {f32x16{0.f}, f32x16{0.f}};
+  const int NC = Dp >> 5;
+  for (int c = 0; c < NC; ++c) {
+    __syncthreads();
+    if (x_blocked) {
+      const float* xb = X + ((base >> 6) * Dp + 32 * c) * 64;
+      for (int s = tid; s < 64 * 32; s += 256) xs[(s & 63) * 33 + (s >> 6)] = xb[s];
+    } else {
+      for (int s = tid; s < 64 * 32; s += 256) {
+        const int rr = s >> 5, kk = s & 31;
+        const int64_t id = rid[rr];
+        xs[rr * 33 + kk] = id >= 0 ? X[id * Dp + 32 * c + kk] : 0.0f;
+      }
+    }
+    if (!trans) {
+      for (int s = tid; s < 32 * WB; s += 256) {
+        const int kk = s >> 7, j = s & 127;
+        bs[kk * (WB + 1) + j] = Q[(int64_t)(32 * c + kk) * Dp + WB * cb + j];
+      }
+    } else {
+      for (int s = tid; s < 32 * WB; s += 256) {
+        const int j = s >> 5, kk = s & 31;
+        bs[kk * (WB + 1) + j] = Q[(int64_t)(WB * cb + j) * Dp + 32 * c + kk];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int C = Cs + t;
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const int kk = 2 * s2 + hi;
+        acc[t] = mfma32(xs[(32 * R + lo) * 33 + kk], bs[kk * (WB + 1) + 32 * C + lo], acc[t]);
+      }
+    }
+  }
+  if (!qpart) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int C = Cs + t;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t id = rid[32 * R + acc_row(q, hi)];
+        if (id >= 0) Y[id * Dp + WB * cb + 32 * C + lo] = acc[t][q];
+      }
+    }
+    return;
+  }
+  // row dots with X over this block's 128 columns
+  float rs[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t id = rid[32 * R + acc_row(q, hi)];
+    float s = 0.0f;
+    if (id >= 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) s += acc[t][q] * X[id * Dp + WB * cb + 32 * (Cs + t) + lo];
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o);  // over the 32 columns of a half
+    rs[q] = s;
+  }
+  if (lo == 0) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) qred[wave >> 1][32 * R + acc_row(q, hi)] = rs[q];
+  }
+  __syncthreads();
+  if (tid < 64 && base + tid < n) qpart[(int64_t)cb * n + base + tid] = qred[0][tid] + qred[1][tid];
+}
+
+// User loss at wide Dp: one wave per user, Dp/32 lanes per history row
+// (8 float4 each), 64*32/Dp rows in flight; u^T G u from the rot_wide_kernel
+// partials summed in column-block order.
+template <int Dp>
+__global__ void __launch_bounds__(256) loss_gather_wide_kernel(LossArgs a) {
+  constexpr int LPR = Dp / 32, NG = 64 / LPR, NB = Dp / WB;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t idx = (int64_t)blockIdx.x * 4 + wave;
+  if (idx >= a.n_rows) return;
+  const int64_t e = a.row_lo + idx;
+  const int64_t p0 = a.row_ptr[e];
+  const int64_t h = a.row_ptr[e + 1] - p0;
+  if (h == 0) return;
+  const int g = lane / LPR, c = lane % LPR;
+  float4 u4[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    u4[q] = *reinterpret_cast<const float4*>(a.U + e * Dp + 4 * (c + LPR * q));
+  float sq = 0.0f;
+  for (int64_t k0 = 0; k0 < h; k0 += NG) {
+    const int64_t k = k0 + g;
+    float d = 0.0f;
+    if (k < h) {
+      const int id = a.col[p0 + k];
+      const float* x = a.V + (int64_t)id * Dp;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(x + 4 * (c + LPR * q));
+        d += v.x * u4[q].x + v.y * u4[q].y + v.z * u4[q].z + v.w * u4[q].w;
+      }
+    }
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) d += __shfl_xor(d, o);
+    if (c == 0 && k < h) {
+      const float t = d - 1.0f;
+      sq = (float)((double)sq + (double)t * (double)t);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+  float qv = 0.0f;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) qv += a.quad[(int64_t)b * a.n_rows + idx];
+  float loss = sq / (float)h + a.beta * qv;
+  if (a.half) loss = (float)((double)loss / 2.0);
+  if (lane == 0) a.out[e] = loss;
+}
+
+int64_t wide_rows_per_block(int64_t n) {
+  int64_t rpb = (n + kWideMaxBlocks - 1) / kWideMaxBlocks;
+  if (rpb < 256) rpb = 256;
+  return (rpb + WR - 1) / WR * WR;
+}
+
+int wide_pairs(int Dp) {
+  const int nb = Dp / WB;
+  return nb * (nb + 1) / 2;
+}
+
+size_t wide_chol_lds_bytes(int Dp) {
+  const int T = Dp >> 5;
+  return sizeof(float) * ((size_t)1024 + (size_t)T * 1024 + 2 * Dp + 8 * 32 + 32 + 4);
+}
+
+}  // namespace
+
+bool wide_dim(int Dp) { return Dp == 512 || Dp == 1024; }
+
+size_t wide_slot_floats(int Dp) {
+  const int T = Dp >> 5;
+  return (size_t)T * (T + 1) / 2 * 1024 + Dp;
+}
+
+int64_t wide_gram_num_blocks(int64_t n) {
+  const int64_t rpb = wide_rows_per_block(n);
+  return (n + rpb - 1) / rpb;
+}
+
+hipError_t launch_wide_gramian(int Dp, const GramArgs& g, hipStream_t s) {
+  if (!wide_dim(Dp)) return hipErrorInvalidValue;
+  const int64_t rpb = wide_rows_per_block(g.n);
+  const int64_t nblk = (g.n + rpb - 1) / rpb;
+  if (nblk == 0) return hipMemsetAsync(g.G, 0, sizeof(float) * Dp * Dp, s);
+  SolveArgs a{};
+  hipLaunchKernelGGL(wide_syrk_kernel<0>, dim3((unsigned)nblk, (unsigned)wide_pairs(Dp)),
+                     dim3(256), 0, s, a, g, Dp, rpb, (int64_t)0, (float*)nullptr);
+  hipLaunchKernelGGL(wide_gram_reduce_kernel, dim3((unsigned)(((int64_t)Dp * Dp + 255) / 256)),
+                     dim3(256), 0, s, g.partials, nblk, g.G, Dp);
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batch,
+                             hipStream_t s) {
+  if (!wide_dim(Dp) || batch <= 0) return hipErrorInvalidValue;
+  if (a.n_rows <= 0) return hipSuccess;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)wide_chol_lds_bytes(1024));
+    if (err != hipSuccess) return err;
+    attr = true;
+  }
+  const bool grad = is_grad_kind(a.kind);
+  GramArgs g{};
+  for (int64_t s0 = 0; s0 < a.n_rows; s0 += batch) {
+    const int64_t nb = std::min<int64_t>(batch, a.n_rows - s0);
+    hipLaunchKernelGGL(wide_syrk_kernel<1>, dim3((unsigned)nb, (unsigned)wide_pairs(Dp)),
+                       dim3(256), 0, s, a, g, Dp, (int64_t)0, s0, ws);
+    if (grad)
+      hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
+    else
+      hipLaunchKernelGGL(wide_chol_kernel, dim3((unsigned)nb), dim3(512),
+                         wide_chol_lds_bytes(Dp), s, a, Dp, s0, ws);
+  }
+  return hipGetLastError();
+}
+
+size_t wide_tridiag_work_floats(int Dp) { return (size_t)2 * Dp * Dp + 2 * (size_t)Dp; }
+
+hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
+                               float* tau, float* work, hipStream_t s) {
+  if (!wide_dim(Dp) || !work) return hipErrorInvalidValue;
+  const int n = Dp;
+  float* A[2] = {work, work + (size_t)n * n};
+  float* P[2] = {work + (size_t)2 * n * n, work + (size_t)2 * n * n + n};
+  const unsigned nb = (unsigned)((n + 15) / 16);
+  for (int k = 0; k < n; ++k) {
+    const float* ain = k == 0 ? G : A[(k - 1) & 1];
+    hipLaunchKernelGGL(tridiag_step_kernel, dim3(nb), dim3(256), 0, s, ain, A[k & 1], n, k,
+                       (const float*)P[(k + 1) & 1], P[k & 1], Vh, tau, tdiag, toff);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_rot(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
+                           const float* Q, int trans, float* Y, int Dp, hipStream_t s,
+                           int x_blocked) {
+  if (!wide_dim(Dp)) return hipErrorInvalidValue;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rot_wide_kernel, dim3((unsigned)((n + 63) / 64), (unsigned)(Dp / WB)),
+                     dim3(256), 0, s, X, rows, r0, n, Q, trans, Y, x_blocked, Dp,
+                     (float*)nullptr);
+  return hipGetLastError();
+}
+
+size_t wide_quad_floats(int Dp, int64_t rows) { return (size_t)(Dp / WB) * (size_t)rows; }
+
+hipError_t launch_wide_user_loss(int Dp, const LossArgs& a, hipStream_t s) {
+  if (!wide_dim(Dp)) return hipErrorInvalidValue;
+  if (a.n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rot_wide_kernel, dim3((unsigned)((a.n_rows + 63) / 64), (unsigned)(Dp / WB)),
+                     dim3(256), 0, s, a.U, (const QueueRec*)nullptr, a.row_lo, a.n_rows, a.G, 0,
+                     (float*)nullptr, 0, Dp, a.quad);
+  const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
+  if (Dp == 512)
+    hipLaunchKernelGGL(loss_gather_wide_kernel<512>, dim3(nb), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(loss_gather_wide_kernel<1024>, dim3(nb), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace frecsys_hip

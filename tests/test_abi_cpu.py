@@ -46,7 +46,10 @@ def test_library_is_gfx950_code_object():
 def test_padded_dim():
     assert [fh.padded_dim(d) for d in (1, 8, 9, 16, 17, 32, 33, 200, 256)] == \
         [8, 8, 16, 16, 32, 32, 64, 224, 256]
-    assert fh.padded_dim(257) == 0
+    # wide dims (csrc/wide.hip): 512 and 1024 only
+    assert [fh.padded_dim(d) for d in (257, 300, 512, 513, 1000, 1024)] == \
+        [512, 512, 512, 1024, 1024, 1024]
+    assert fh.padded_dim(1025) == 0
 
 
 def test_partition_nnz_balanced():

@@ -231,5 +231,5 @@ def test_bad_csr_rejected(quirk_data):
 
 def test_unsupported_dim():
     with pytest.raises(fh.FrecsysError) as ei:
-        fh.Context(300, 10, 10)
+        fh.Context(1025, 10, 10)
     assert ei.value.code == fh.ERR_UNSUPPORTED
