@@ -75,32 +75,48 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return s;
 }
 
-// MODE 0: partial Gramian of rows [r0, r1) (operand weight g.w);
-// MODE 1: assembly of entity order[pos0 + blockIdx.x] into its workspace slot.
+// XCD-aware grid: workgroup b runs on XCD b % 8 (round-robin dispatch), so
+// the P block pairs of one unit (entity / row block) are given consecutive
+// slots of ONE XCD's sequence -- they run together and the unit's rows are
+// fetched from HBM once into that XCD's L2 instead of once per pair.
+__device__ __forceinline__ bool xcd_unit(int P, int64_t n_units, int64_t& unit, int& pidx) {
+  const int64_t bid = blockIdx.x;
+  const int64_t s = bid >> 3;
+  pidx = (int)(s % P);
+  unit = (s / P) * 8 + (bid & 7);
+  return unit < n_units;
+}
+
+// MODE 0: partial Gramian of the unit's rows [r0, r1) (operand weight g.w);
+// MODE 1: assembly of entity order[pos0 + unit] into its workspace slot.
 template <int MODE>
 __global__ void __launch_bounds__(256)
-    wide_syrk_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws) {
+    wide_syrk_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws,
+                     int64_t n_units) {
   __shared__ __attribute__((aligned(16))) float xa[2][WR * WB];
   __shared__ __attribute__((aligned(16))) float xb[2][WR * WB];
   __shared__ int ring_id[WRING * WR];
   __shared__ float ring_sa[WRING * WR], ring_bw[WRING * WR];
   const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = Dp >> 5, NT = T * (T + 1) / 2, NB = Dp / WB;
+  int64_t unit;
+  int pidx;
+  if (!xcd_unit(NB * (NB + 1) / 2, n_units, unit, pidx)) return;
   int BI, BJ;
-  pair_of(blockIdx.y, BI, BJ);
+  pair_of(pidx, BI, BJ);
   const bool dgp = BI == BJ;
-  const int T = Dp >> 5, NT = T * (T + 1) / 2;
   const int kind = a.kind;
   const bool vk = MODE == 1 && is_v_kind(kind);
 
   int64_t r0 = 0, nrow = 0, e = 0, h = 0, p0 = 0;
   if (MODE == 0) {
-    r0 = g.row0 + (int64_t)blockIdx.x * rpb;
+    r0 = g.row0 + unit * rpb;
     int64_t r1 = r0 + rpb;
     if (r1 > g.row0 + g.n) r1 = g.row0 + g.n;
     nrow = r1 > r0 ? r1 - r0 : 0;
   } else {
-    const QueueRec rec = a.order[pos0 + blockIdx.x];
+    const QueueRec rec = a.order[pos0 + unit];
     e = rec.entity;
     h = rec.h;
     p0 = rec.p0;
@@ -263,7 +279,7 @@ __global__ void __launch_bounds__(256)
   }
 
   if (MODE == 0) {
-    float* P = g.partials + (int64_t)blockIdx.x * NT * 1024;
+    float* P = g.partials + unit * NT * 1024;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (!dgp || j <= wave) {
@@ -277,7 +293,7 @@ __global__ void __launch_bounds__(256)
   }
 
   // epilogue: finish A (per kind, as solve.hip) into the workspace tiles
-  float* slot = ws + (int64_t)blockIdx.x * ((int64_t)NT * 1024 + Dp);
+  float* slot = ws + unit * ((int64_t)NT * 1024 + Dp);
   const float us = omega / hf;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -401,18 +417,35 @@ __global__ void __launch_bounds__(512)
     }
     __syncthreads();
     // trailing update A_IJ -= L_Ip L_Jp^T, p < J <= I
+    // (software-pipelined: the next tile's loads are in flight under this
+    // tile's MFMAs)
     const int m = T - 1 - p, ntr = m * (m + 1) / 2;
-#pragma unroll 1
-    for (int tt = wave; tt < ntr; tt += NW) {
+    auto tile_ij = [&](int tt, int& I, int& J) {
       int Ir = 0;
       while ((Ir + 1) * (Ir + 2) / 2 <= tt) ++Ir;
-      const int Jr = tt - Ir * (Ir + 1) / 2;
-      const int I = p + 1 + Ir, J = p + 1 + Jr;
-      float* Ag = gtile(I, J);
-      f32x16 v;
+      I = p + 1 + Ir;
+      J = p + 1 + tt - Ir * (Ir + 1) / 2;
+    };
+    int In = 0, Jn = 0;
+    f32x16 vn;
+    if (wave < ntr) {
+      tile_ij(wave, In, Jn);
+      const float* An = gtile(In, Jn);
 #pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = Ag[acc_row(q, hi) * 32 + lo];
+      for (int q = 0; q < 16; ++q) vn[q] = An[acc_row(q, hi) * 32 + lo];
+    }
+#pragma unroll 1
+    for (int tt = wave; tt < ntr; tt += NW) {
+      const int I = In, J = Jn;
+      const f32x16 v = vn;
+      if (tt + NW < ntr) {
+        tile_ij(tt + NW, In, Jn);
+        const float* An = gtile(In, Jn);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) vn[q] = An[acc_row(q, hi) * 32 + lo];
+      }
       const f32x16 u = tile_pqT(pan + I * 1024, pan + J * 1024, lo, hi);
+      float* Ag = gtile(I, J);
 #pragma unroll
       for (int q = 0; q < 16; ++q) Ag[acc_row(q, hi) * 32 + lo] = v[q] - u[q];
     }
@@ -722,6 +755,8 @@ int wide_pairs(int Dp) {
   return nb * (nb + 1) / 2;
 }
 
+unsigned xcd_grid(int64_t n_units, int P) { return (unsigned)(((n_units + 7) / 8) * 8 * P); }
+
 size_t wide_chol_lds_bytes(int Dp) {
   const int T = Dp >> 5;
   return sizeof(float) * ((size_t)1024 + (size_t)T * 1024 + 2 * Dp + 8 * 32 + 32 + 4);
@@ -747,8 +782,8 @@ hipError_t launch_wide_gramian(int Dp, const GramArgs& g, hipStream_t s) {
   const int64_t nblk = (g.n + rpb - 1) / rpb;
   if (nblk == 0) return hipMemsetAsync(g.G, 0, sizeof(float) * Dp * Dp, s);
   SolveArgs a{};
-  hipLaunchKernelGGL(wide_syrk_kernel<0>, dim3((unsigned)nblk, (unsigned)wide_pairs(Dp)),
-                     dim3(256), 0, s, a, g, Dp, rpb, (int64_t)0, (float*)nullptr);
+  hipLaunchKernelGGL(wide_syrk_kernel<0>, dim3(xcd_grid(nblk, wide_pairs(Dp))), dim3(256), 0, s, a,
+                     g, Dp, rpb, (int64_t)0, (float*)nullptr, nblk);
   hipLaunchKernelGGL(wide_gram_reduce_kernel, dim3((unsigned)(((int64_t)Dp * Dp + 255) / 256)),
                      dim3(256), 0, s, g.partials, nblk, g.G, Dp);
   return hipGetLastError();
@@ -770,8 +805,8 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
   GramArgs g{};
   for (int64_t s0 = 0; s0 < a.n_rows; s0 += batch) {
     const int64_t nb = std::min<int64_t>(batch, a.n_rows - s0);
-    hipLaunchKernelGGL(wide_syrk_kernel<1>, dim3((unsigned)nb, (unsigned)wide_pairs(Dp)),
-                       dim3(256), 0, s, a, g, Dp, (int64_t)0, s0, ws);
+    hipLaunchKernelGGL(wide_syrk_kernel<1>, dim3(xcd_grid(nb, wide_pairs(Dp))), dim3(256), 0, s,
+                       a, g, Dp, (int64_t)0, s0, ws, nb);
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
     else
