@@ -160,6 +160,14 @@ int frecsys_solve_side(frecsys_ctx* ctx, int32_t side,
  * on device); for USER it is gathered across ranks first. */
 int frecsys_user_loss(frecsys_ctx* ctx, int32_t side, float beta, int32_t half,
                       float* host_out);
+/* Fold-in evaluation ranking (replaces the scoring + top-K of
+ * EvaluateDatasetInternal / EvaluateUser, recommender.h:78-199): for every
+ * row r of the EVAL side, scores s = V u_r over all items (fp32), the items
+ * of row r's own EVAL history set to lowest() (the reference's `exclude`,
+ * its fold-in history), then the k best items by descending score, ties by
+ * ascending item id (the reference leaves tie order unspecified), into
+ * topk[r*k .. r*k+k) (host int32).  1 <= k <= 1024, k <= items. */
+int frecsys_eval_topk(frecsys_ctx* ctx, int32_t k, int32_t* topk);
 /* Block until all queued device work is done (all calls already do). */
 int frecsys_synchronize(frecsys_ctx* ctx);
 

@@ -99,6 +99,10 @@ struct frecsys_ctx {
   // wide dims (Dp = 512 / 1024): tridiagonalisation work, d-space workspace
   float* tri_work = nullptr;
   size_t cap_tri_work = 0;
+  float* d_scores = nullptr;     // evaluation: [batch][items] scores
+  size_t cap_scores = 0;
+  int32_t* d_topk = nullptr;     // [eval rows][k]
+  size_t cap_topk = 0;
   float* wide_ws = nullptr;      // [wide batch][wide_slot_floats(Dp)]
   size_t cap_wide_ws = 0;
   int64_t wide_ws_mb = 4096;     // FRECSYS_WIDE_WS_MB: workspace budget
@@ -552,6 +556,8 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (c->dual_table) (void)hipFree(c->dual_table);
   if (c->tri_work) (void)hipFree(c->tri_work);
   if (c->wide_ws) (void)hipFree(c->wide_ws);
+  if (c->d_scores) (void)hipFree(c->d_scores);
+  if (c->d_topk) (void)hipFree(c->d_topk);
   if (c->d_split) (void)hipFree(c->d_split);
   if (c->d_work) (void)hipFree(c->d_work);
   if (c->d_slabs) (void)hipFree(c->d_slabs);
@@ -1092,6 +1098,35 @@ int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, fl
       HIP_TRY(c, hipMemcpyAsync(host_out, c->d_loss, sizeof(float) * rows, hipMemcpyDeviceToHost,
                                 c->stream));
   }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_eval_topk(frecsys_ctx* c, int32_t k, int32_t* topk) {
+  if (!c || !topk) return fail(c, FRECSYS_ERR_INVALID, "eval_topk: bad arguments");
+  if (!c->rp[2] || !c->emb[2]) return fail(c, FRECSYS_ERR_INVALID, "eval_topk: no EVAL side loaded");
+  const int64_t n = c->n[2], m = c->n[1];
+  if (k < 1 || k > 1024 || k > m)
+    return fail(c, FRECSYS_ERR_INVALID, "eval_topk: k must be in [1, min(1024, items)]");
+  if (n == 0) return FRECSYS_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  // scores in batches of rows bounded to 1 GiB of workspace
+  const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(n, ((int64_t)1 << 28) / m));
+  int rc = ensure(c, &c->d_scores, &c->cap_scores, (size_t)nb * m);
+  if (rc) return rc;
+  rc = ensure(c, &c->d_topk, &c->cap_topk, (size_t)n * k);
+  if (rc) return rc;
+  {
+    ScopedTimer t(c, "eval_topk");
+    for (int64_t r0 = 0; r0 < n; r0 += nb) {
+      const int64_t cnt = std::min(nb, n - r0);
+      HIP_TRY(c, launch_eval_topk(c->emb[2], r0, cnt, c->emb[1], m, c->Dp, c->rp[2], c->col[2], k,
+                                  c->d_scores, c->d_topk + r0 * k, c->stream));
+    }
+    t.stop();
+  }
+  HIP_TRY(c, hipMemcpyAsync(topk, c->d_topk, sizeof(int32_t) * n * k, hipMemcpyDeviceToHost,
+                            c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FRECSYS_OK;
 }

@@ -155,6 +155,12 @@ __host__ __device__ inline int64_t blk_t(int64_t p, int j, int k, int Dp) {
 }
 hipError_t launch_gramian(int Dp, const GramArgs& a, hipStream_t s);
 
+// Fold-in scoring + top-k (topk.hip): rows r0..r0+n-1 of X against the m
+// rows of Y; S: [n][m] workspace; out: [n][k].
+hipError_t launch_eval_topk(const float* X, int64_t r0, int64_t n, const float* Y, int64_t m,
+                            int Dp, const int64_t* row_ptr, const int32_t* col, int k, float* S,
+                            int32_t* out, hipStream_t s);
+
 // Wide dims, Dp = 512 / 1024 (wide.hip).  d-space solve with A in an HBM
 // workspace ([batch][wide_slot_floats(Dp)]), entities a.order[0..n_rows)
 // in batches; Gramian by 128x128 block pairs; per-step tridiagonalisation

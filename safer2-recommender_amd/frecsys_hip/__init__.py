@@ -34,6 +34,7 @@ EXPORTS = (
     "frecsys_get_embeddings", "frecsys_init_embeddings", "frecsys_snapshot",
     "frecsys_gramian", "frecsys_set_gramian", "frecsys_solve_side", "frecsys_user_loss",
     "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset", "frecsys_debug_basis",
+    "frecsys_eval_topk",
 )
 
 
@@ -95,6 +96,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, P]),
         "frecsys_timing_reset": (ctypes.c_int, [P]),
         "frecsys_debug_basis": (ctypes.c_int, [P, I32, P, P, P]),
+        "frecsys_eval_topk": (ctypes.c_int, [P, I32, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -250,6 +252,13 @@ class Context:
 
     def timing_reset(self):
         self._check(self.lib.frecsys_timing_reset(self.h))
+
+    def eval_topk(self, k: int):
+        """[EVAL rows, k] int32: best k items per fold-in row, history excluded,
+        score descending, ties by item id."""
+        out = np.zeros((self.n[SIDE_EVAL], k), dtype=np.int32)
+        self._check(self.lib.frecsys_eval_topk(self.h, k, _ptr(out)))
+        return out
 
     def debug_basis(self, side: int):
         """(Q, diag, sub) with G[side] = Q T Q^T (diagnostic, Dp >= 64)."""

@@ -134,6 +134,13 @@ class DeviceContext {
     if (side != EVAL) bump(side);
   }
 
+  // Best k items per EVAL row (history excluded), [rows][k] (GPU scoring + top-k).
+  std::vector<int32_t> EvalTopK(int k) {
+    std::vector<int32_t> out((size_t)n_[EVAL] * k);
+    check(frecsys_eval_topk(ctx_, k, out.data()), "eval_topk");
+    return out;
+  }
+
   // Per-user loss of `side` (USER or EVAL) against ITEM / G[ITEM].
   void UserLoss(int side, float beta, bool half, float* host_out) {
     check(frecsys_user_loss(ctx_, side, beta, half ? 1 : 0, host_out), "user_loss");

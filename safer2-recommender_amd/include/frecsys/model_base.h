@@ -54,8 +54,11 @@ class DeviceModel : public Recommender {
  protected:
   virtual void OnEmbeddingsSet() {}
 
-  // Fold-in + scoring (ials.h:148-185 and its model variants): project the
-  // users of `data` with `params` on the GPU, then rank on host.
+  // Fold-in + evaluation (ials.h:148-185 and its model variants, then
+  // EvaluateDatasetInternal / EvaluateUser, recommender.h:78-199): project
+  // the users of `data` with `params`, score every item, exclude each user's
+  // fold-in history and rank -- all on the GPU (frecsys_eval_topk); Recall /
+  // NDCG of the k_list cut-offs on host.
   EvaluationResult FoldInEvaluate(const VectorXi& k_list, const VectorXf& alpha_list,
                                   const Dataset& data, const SpMatrix& eval_by_user,
                                   const frecsys_solve_params& params) {
@@ -64,27 +67,24 @@ class DeviceModel : public Recommender {
     data.compact_users(&ids, &csr);
     dev_->LoadEval(csr);
     dev_->Solve(DeviceContext::EVAL, params);
-    const MatrixXf Ue = dev_->Get(DeviceContext::EVAL);
-    const MatrixXf V = dev_->Get(DeviceContext::ITEM);
+    const int max_k = std::min<int>(k_list.maxCoeff(), (int)num_items_);
+    const std::vector<int32_t> top = dev_->EvalTopK(max_k);
     std::unordered_map<int, int> user_to_ind;
     for (size_t i = 0; i < ids.size(); ++i) user_to_ind[ids[i]] = (int)i;
-    std::unordered_map<int, int> row_of;
-    int n = 0;
-    for (const auto& kv : eval_by_user) row_of[kv.first] = n++;
-    const int64_t d = dim_;
-    return EvaluateDatasetInternal(
-        (int)num_items_, k_list, alpha_list, row_of, data, eval_by_user,
-        [&](const int user_id, const SpVector&) {
-          VectorXf s(V.rows());
-          const float* u = Ue.row(user_to_ind.at(user_id));
-          for (int64_t i = 0; i < V.rows(); ++i) {
-            const float* v = V.row(i);
-            float t = 0.f;
-            for (int64_t k = 0; k < d; ++k) t += v[k] * u[k];
-            s[i] = t;
-          }
-          return s;
-        });
+    const int64_t nk = k_list.size();
+    const int64_t nu = (int64_t)eval_by_user.size();
+    MatrixXf recall = MatrixXf::Zero(nu, nk), ndcg = MatrixXf::Zero(nu, nk);
+    int row = 0;
+    for (const auto& kv : eval_by_user) {
+      const int32_t* t = top.data() + (size_t)user_to_ind.at(kv.first) * max_k;
+      const UserEvaluationResult m = RankMetrics(k_list, t, max_k, kv.second);
+      for (int64_t i = 0; i < nk; ++i) {
+        recall(row, i) = m.recall[i];
+        ndcg(row, i) = m.ndcg[i];
+      }
+      ++row;
+    }
+    return EvaluationResult{k_list, alpha_list, recall, ndcg};
   }
 
   // Initialize() bookkeeping of ERM-MF / CVaR-MF / SAFER2

@@ -72,9 +72,16 @@ class Recommender {
     auto greater = [&scores](size_t a, size_t b) { return scores[a] > scores[b]; };
     std::nth_element(topk.begin(), topk.begin() + max_k, topk.end(), greater);
     std::stable_sort(topk.begin(), topk.begin() + max_k, greater);
+    (void)num_items;
+    return RankMetrics(k_list, topk.data(), max_k, ground_truth);
+  }
+
+  // Recall@K and NDCG@K of a ranked list (recommender.h:152-182).
+  template <typename Id>
+  static UserEvaluationResult RankMetrics(const VectorXi& k_list, const Id* topk, int max_k,
+                                          const SpVector& ground_truth) {
     std::set<int> gt;
     for (const auto& p : ground_truth) gt.insert(p.first);
-    (void)num_items;
     const int64_t nk = k_list.size();
     UserEvaluationResult r{VectorXf(nk), VectorXf(nk)};
     for (int64_t i = 0; i < nk; ++i) {
