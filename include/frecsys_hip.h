@@ -168,6 +168,15 @@ int frecsys_user_loss(frecsys_ctx* ctx, int32_t side, float beta, int32_t half,
  * ascending item id (the reference leaves tie order unspecified), into
  * topk[r*k .. r*k+k) (host int32).  1 <= k <= 1024, k <= items. */
 int frecsys_eval_topk(frecsys_ctx* ctx, int32_t k, int32_t* topk);
+/* Train-loss diagnostics (ComputeLosses / PrintLosses, ials.h:226-305,
+ * safer2.h:337-413), all rows of both sides on every rank: observed = sum
+ * over every USER-side interaction of (v.u - 1)^2 (per-user fp32 sums,
+ * total in double), unobserved = sum_ij (U^T U)_ij (V^T V)_ij (unweighted
+ * Gramians, double), and the squared row norms of U and V (host [n_users]
+ * and [n_items]).  Any output pointer may be NULL.  The Gramian slots used
+ * by the solves are left untouched. */
+int frecsys_train_stats(frecsys_ctx* ctx, double* observed, double* unobserved,
+                        float* user_norm2, float* item_norm2);
 /* Block until all queued device work is done (all calls already do). */
 int frecsys_synchronize(frecsys_ctx* ctx);
 

@@ -99,6 +99,12 @@ struct frecsys_ctx {
   // wide dims (Dp = 512 / 1024): tridiagonalisation work, d-space workspace
   float* tri_work = nullptr;
   size_t cap_tri_work = 0;
+  float* d_rows = nullptr;       // train stats: per-row values
+  size_t cap_rows = 0;
+  float* d_gstat = nullptr;      // train stats: U^T U, V^T V
+  size_t cap_gstat = 0;
+  double* d_dot = nullptr;
+  size_t cap_dot = 0;
   float* d_scores = nullptr;     // evaluation: [batch][items] scores
   size_t cap_scores = 0;
   int32_t* d_topk = nullptr;     // [eval rows][k]
@@ -557,6 +563,9 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (c->tri_work) (void)hipFree(c->tri_work);
   if (c->wide_ws) (void)hipFree(c->wide_ws);
   if (c->d_scores) (void)hipFree(c->d_scores);
+  if (c->d_rows) (void)hipFree(c->d_rows);
+  if (c->d_gstat) (void)hipFree(c->d_gstat);
+  if (c->d_dot) (void)hipFree(c->d_dot);
   if (c->d_topk) (void)hipFree(c->d_topk);
   if (c->d_split) (void)hipFree(c->d_split);
   if (c->d_work) (void)hipFree(c->d_work);
@@ -1128,6 +1137,73 @@ int frecsys_eval_topk(frecsys_ctx* c, int32_t k, int32_t* topk) {
   HIP_TRY(c, hipMemcpyAsync(topk, c->d_topk, sizeof(int32_t) * n * k, hipMemcpyDeviceToHost,
                             c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_train_stats(frecsys_ctx* c, double* observed, double* unobserved,
+                        float* user_norm2, float* item_norm2) {
+  if (!c) return fail(c, FRECSYS_ERR_INVALID, "train_stats: null ctx");
+  if (observed && !c->rp[0]) return fail(c, FRECSYS_ERR_INVALID, "train_stats: no USER CSR");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int64_t nu = c->n[0], ni = c->n[1];
+  const int Dp = c->Dp;
+  int rc = ensure(c, &c->d_rows, &c->cap_rows, (size_t)std::max<int64_t>(std::max(nu, ni), 1));
+  if (rc) return rc;
+  ScopedTimer t(c, "train_stats");
+  if (observed) {
+    LossArgs a{};
+    a.row_ptr = c->rp[0];
+    a.col = c->col[0];
+    a.row_lo = 0;
+    a.n_rows = nu;
+    a.U = c->emb[0];
+    a.V = c->emb[1];
+    a.G = c->gram[1];
+    a.out = c->d_rows;
+    a.raw = 1;
+    HIP_TRY(c, hipMemsetAsync(c->d_rows, 0, sizeof(float) * std::max<int64_t>(nu, 1), c->stream));
+    HIP_TRY(c, launch_user_loss(Dp, a, c->stream));
+    std::vector<float> h((size_t)nu);
+    if (nu)
+      HIP_TRY(c, hipMemcpyAsync(h.data(), c->d_rows, sizeof(float) * nu, hipMemcpyDeviceToHost,
+                                c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    double s = 0.0;
+    for (float v : h) s += (double)v;
+    *observed = s;
+  }
+  if (unobserved) {
+    rc = ensure(c, &c->d_gstat, &c->cap_gstat, (size_t)2 * Dp * Dp);
+    if (rc) return rc;
+    rc = ensure(c, &c->d_partials, &c->cap_partials,
+                gram_workspace_floats(Dp, std::max<int64_t>(std::max(nu, ni), 1)));
+    if (rc) return rc;
+    rc = ensure(c, &c->d_dot, &c->cap_dot, 1);
+    if (rc) return rc;
+    for (int s = 0; s < 2; ++s) {
+      GramArgs g{};
+      g.X = c->emb[s];
+      g.row0 = 0;
+      g.n = c->n[s];
+      g.w = nullptr;
+      g.partials = c->d_partials;
+      g.G = c->d_gstat + (size_t)s * Dp * Dp;
+      HIP_TRY(c, launch_gramian(Dp, g, c->stream));
+    }
+    HIP_TRY(c, launch_gram_dot(c->d_gstat, c->d_gstat + (size_t)Dp * Dp, Dp, c->d_dot, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(unobserved, c->d_dot, sizeof(double), hipMemcpyDeviceToHost,
+                              c->stream));
+  }
+  for (int s = 0; s < 2; ++s) {
+    float* host = s == 0 ? user_norm2 : item_norm2;
+    if (!host || c->n[s] == 0) continue;
+    HIP_TRY(c, launch_row_norm2(c->emb[s], c->n[s], Dp, c->d_rows, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(host, c->d_rows, sizeof(float) * c->n[s], hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  t.stop();
   return FRECSYS_OK;
 }
 

@@ -74,6 +74,7 @@ struct LossArgs {
   int half;
   float* out;            // [rows of side]
   float* quad;           // [rows of side] scratch: u^T G u (Dp >= 32)
+  int raw;               // 1: out[e] = sum_j (x_j . u - 1)^2 only (train stats)
 };
 
 // Number of workgroups / partial slabs the Gramian of n rows uses.
@@ -182,6 +183,10 @@ size_t wide_quad_floats(int Dp, int64_t rows);
 hipError_t launch_wide_user_loss(int Dp, const LossArgs& a, hipStream_t s);
 hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s);
 hipError_t launch_zero_gram(int Dp, float* G, hipStream_t s);
+// Train-loss diagnostics: out[r] = ||X[r]||^2 for n rows; dot = sum_ij A_ij B_ij
+// (double, Dp x Dp).
+hipError_t launch_row_norm2(const float* X, int64_t n, int Dp, float* out, hipStream_t s);
+hipError_t launch_gram_dot(const float* A, const float* B, int Dp, double* dot, hipStream_t s);
 
 // Padded leading dimension for a logical dimension (8, 16, multiples of 32
 // up to 256, then 512 and 1024).  Returns 0 when unsupported.

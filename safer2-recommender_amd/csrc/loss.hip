@@ -69,6 +69,10 @@ __global__ void __launch_bounds__(256) user_loss_kernel(LossArgs a) {
     }
   }
   sq = wave_sum(sq);
+  if (a.raw) {
+    if (lane == 0) a.out[e] = sq;
+    return;
+  }
   float loss = sq / (float)h;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -199,6 +203,10 @@ __global__ void __launch_bounds__(256) loss_gather_kernel(LossArgs a) {
     }
   }
   sq = wave_sum(sq);
+  if (a.raw) {
+    if (lane == 0) a.out[e] = sq;
+    return;
+  }
   float loss = sq / (float)h + a.beta * a.quad[e];
   if (a.half) loss = (float)((double)loss / 2.0);
   if (lane == 0) a.out[e] = loss;
@@ -208,7 +216,7 @@ template <int NCT>
 hipError_t launch2(const LossArgs& a, hipStream_t s) {
   constexpr int Dp = 32 * NCT;
   const unsigned nq = (unsigned)((a.n_rows + 63) / 64);
-  hipLaunchKernelGGL(quad_kernel<NCT>, dim3(nq), dim3(256), 0, s, a);
+  if (!a.raw) hipLaunchKernelGGL(quad_kernel<NCT>, dim3(nq), dim3(256), 0, s, a);
   const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
   hipLaunchKernelGGL(loss_gather_kernel<Dp>, dim3(nb), dim3(256), 0, s, a);
   return hipGetLastError();
@@ -221,7 +229,50 @@ hipError_t launch(const LossArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ||X[r]||^2, one wave per row.
+__global__ void __launch_bounds__(256) row_norm2_kernel(const float* __restrict__ X, int64_t n,
+                                                        int Dp, float* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  float s = 0.0f;
+  for (int j = lane; j < Dp; j += 64) {
+    const float v = X[r * Dp + j];
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[r] = s;
+}
+
+// sum_ij A_ij B_ij in double, one workgroup.
+__global__ void __launch_bounds__(256) gram_dot_kernel(const float* __restrict__ A,
+                                                       const float* __restrict__ B, int Dp,
+                                                       double* __restrict__ dot) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < (int64_t)Dp * Dp; i += 256) s += (double)A[i] * (double)B[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dot[0] = red[0];
+}
+
 }  // namespace
+
+hipError_t launch_row_norm2(const float* X, int64_t n, int Dp, float* out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(row_norm2_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, X, n, Dp,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_dot(const float* A, const float* B, int Dp, double* dot, hipStream_t s) {
+  hipLaunchKernelGGL(gram_dot_kernel, dim3(1), dim3(256), 0, s, A, B, Dp, dot);
+  return hipGetLastError();
+}
 
 hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;

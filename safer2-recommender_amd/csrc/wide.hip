@@ -736,6 +736,10 @@ __global__ void __launch_bounds__(256) loss_gather_wide_kernel(LossArgs a) {
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) sq += __shfl_xor(sq, o);
+  if (a.raw) {
+    if (lane == 0) a.out[e] = sq;
+    return;
+  }
   float qv = 0.0f;
 #pragma unroll
   for (int b = 0; b < NB; ++b) qv += a.quad[(int64_t)b * a.n_rows + idx];
@@ -849,9 +853,11 @@ size_t wide_quad_floats(int Dp, int64_t rows) { return (size_t)(Dp / WB) * (size
 hipError_t launch_wide_user_loss(int Dp, const LossArgs& a, hipStream_t s) {
   if (!wide_dim(Dp)) return hipErrorInvalidValue;
   if (a.n_rows <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rot_wide_kernel, dim3((unsigned)((a.n_rows + 63) / 64), (unsigned)(Dp / WB)),
-                     dim3(256), 0, s, a.U, (const QueueRec*)nullptr, a.row_lo, a.n_rows, a.G, 0,
-                     (float*)nullptr, 0, Dp, a.quad);
+  if (!a.raw)
+    hipLaunchKernelGGL(rot_wide_kernel,
+                       dim3((unsigned)((a.n_rows + 63) / 64), (unsigned)(Dp / WB)), dim3(256), 0,
+                       s, a.U, (const QueueRec*)nullptr, a.row_lo, a.n_rows, a.G, 0,
+                       (float*)nullptr, 0, Dp, a.quad);
   const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
   if (Dp == 512)
     hipLaunchKernelGGL(loss_gather_wide_kernel<512>, dim3(nb), dim3(256), 0, s, a);

@@ -34,7 +34,7 @@ EXPORTS = (
     "frecsys_get_embeddings", "frecsys_init_embeddings", "frecsys_snapshot",
     "frecsys_gramian", "frecsys_set_gramian", "frecsys_solve_side", "frecsys_user_loss",
     "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset", "frecsys_debug_basis",
-    "frecsys_eval_topk",
+    "frecsys_eval_topk", "frecsys_train_stats",
 )
 
 
@@ -97,6 +97,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_timing_reset": (ctypes.c_int, [P]),
         "frecsys_debug_basis": (ctypes.c_int, [P, I32, P, P, P]),
         "frecsys_eval_topk": (ctypes.c_int, [P, I32, P]),
+        "frecsys_train_stats": (ctypes.c_int, [P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -259,6 +260,16 @@ class Context:
         out = np.zeros((self.n[SIDE_EVAL], k), dtype=np.int32)
         self._check(self.lib.frecsys_eval_topk(self.h, k, _ptr(out)))
         return out
+
+    def train_stats(self):
+        """(observed, unobserved, ||U_r||^2, ||V_r||^2): ComputeLosses' parts."""
+        obs = ctypes.c_double(0.0)
+        unobs = ctypes.c_double(0.0)
+        un = np.zeros(self.n[SIDE_USER], dtype=np.float32)
+        vn = np.zeros(self.n[SIDE_ITEM], dtype=np.float32)
+        self._check(self.lib.frecsys_train_stats(self.h, ctypes.byref(obs), ctypes.byref(unobs),
+                                                 _ptr(un), _ptr(vn)))
+        return obs.value, unobs.value, un, vn
 
     def debug_basis(self, side: int):
         """(Q, diag, sub) with G[side] = Q T Q^T (diagnostic, Dp >= 64)."""

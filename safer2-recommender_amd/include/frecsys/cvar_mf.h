@@ -54,6 +54,7 @@ class CVaRMFRecommender : public detail::DeviceModel {
 
   void Train(const Dataset& data) override {
     dev_->LoadTraining(data);
+    PrintWeightedLosses(data, regularization_, unobserved_weight_, alpha_);  // cvar_mf.h:277
     const Csr& uc = data.user_csr();
     for (int64_t u = 0; u < uc.rows() && u < num_users_; ++u)  // cvar_mf.h:597-642
       if (uc.len(u)) dual_weight_[u] = (float)((user_loss_[u] - prev_xi_) >= 0);

@@ -134,6 +134,11 @@ class DeviceContext {
     if (side != EVAL) bump(side);
   }
 
+  // ComputeLosses parts on the GPU (frecsys_train_stats).
+  void TrainStats(double* observed, double* unobserved, float* user_norm2, float* item_norm2) {
+    check(frecsys_train_stats(ctx_, observed, unobserved, user_norm2, item_norm2), "train_stats");
+  }
+
   // Best k items per EVAL row (history excluded), [rows][k] (GPU scoring + top-k).
   std::vector<int32_t> EvalTopK(int k) {
     std::vector<int32_t> out((size_t)n_[EVAL] * k);

@@ -59,7 +59,7 @@ class ERMMFRecommender : public detail::DeviceModel {
 
   void Train(const Dataset& data) override {
     dev_->LoadTraining(data);
-    if (print_trainstats_) LOG(INFO) << "(train-loss diagnostics: see SAFER2 PrintLosses)";
+    PrintWeightedLosses(data, regularization_, unobserved_weight_, alpha_);  // erm_mf.h:258
     frecsys_solve_params pu = solve_params(FRECSYS_KIND_WEIGHTED_U, regularization_,
                                            unobserved_weight_);
     pu.entity_weight = dual_weight_.data();

@@ -76,19 +76,18 @@ class IALSRecommender : public detail::DeviceModel {
     if (!print_trainstats_) return;
     const auto t0 = std::chrono::steady_clock::now();
     const LossParts lp = ComputeLossParts(data);
-    const MatrixXf U = dev_->Get(DeviceContext::USER), V = dev_->Get(DeviceContext::ITEM);
     const Csr& uc = data.user_csr();
     const Csr& ic = data.item_csr();
     double loss_reg = 0.0, reg_user_now = 0.0, reg_item_now = 0.0;
     for (int64_t u = 0; u < uc.rows(); ++u) {
       if (!uc.len(u)) continue;
-      const double n2 = RowSqNorm(U, u);
+      const double n2 = lp.user_norm2[u];
       loss_reg += n2 * RegularizationValue((int)uc.len(u), (int)num_items_);
       reg_user_now += n2;
     }
     for (int64_t i = 0; i < ic.rows(); ++i) {
       if (!ic.len(i)) continue;
-      const double n2 = RowSqNorm(V, i);
+      const double n2 = lp.item_norm2[i];
       loss_reg += n2 * RegularizationValue((int)ic.len(i), (int)num_users_);
       reg_item_now += n2;
     }

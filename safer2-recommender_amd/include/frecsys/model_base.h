@@ -112,33 +112,56 @@ class DeviceModel : public Recommender {
     LOG(INFO) << "VaR: " << -vals[Q] << " CVaR: " << loss / (float)Q;
   }
 
-  // Train-loss diagnostics (ials.h:226-305, safer2.h:337-413).  Host-side
-  // diagnostics over downloaded embeddings; counted in Train() time like
-  // the reference's (run_model flag --print_train_stats).
+  // Train-loss diagnostics (ials.h:226-305, safer2.h:337-413): the
+  // observed / unobserved sums and the squared row norms of U and V, computed
+  // on the GPU (frecsys_train_stats); counted in Train() time like the
+  // reference's (run_model flag --print_train_stats, default on).
   struct LossParts {
-    double observed = 0, reg_user_now = 0, reg_item_now = 0, unobserved = 0;
+    double observed = 0, unobserved = 0;
+    std::vector<float> user_norm2, item_norm2;
   };
   LossParts ComputeLossParts(const Dataset& data) {
+    (void)data;
     LossParts lp;
-    const MatrixXf U = dev_->Get(DeviceContext::USER), V = dev_->Get(DeviceContext::ITEM);
-    const Csr& u = data.user_csr();
-    float obs = 0.f;
-    for (int64_t r = 0; r < u.rows(); ++r)
-      for (int64_t k = u.ptr[r]; k < u.ptr[r + 1]; ++k) {
-        float p = 0.f;
-        for (int j = 0; j < dim_; ++j) p += V(u.col[k], j) * U(r, j);
-        obs += (p - 1.0f) * (p - 1.0f);
-      }
-    lp.observed = obs;
-    std::vector<double> gu((size_t)dim_ * dim_, 0.0), gv((size_t)dim_ * dim_, 0.0);
-    for (int64_t r = 0; r < U.rows(); ++r)
-      for (int i = 0; i < dim_; ++i)
-        for (int j = 0; j < dim_; ++j) gu[(size_t)i * dim_ + j] += (double)U(r, i) * U(r, j);
-    for (int64_t r = 0; r < V.rows(); ++r)
-      for (int i = 0; i < dim_; ++i)
-        for (int j = 0; j < dim_; ++j) gv[(size_t)i * dim_ + j] += (double)V(r, i) * V(r, j);
-    for (size_t i = 0; i < gu.size(); ++i) lp.unobserved += gu[i] * gv[i];
+    lp.user_norm2.resize((size_t)num_users_);
+    lp.item_norm2.resize((size_t)num_items_);
+    dev_->TrainStats(&lp.observed, &lp.unobserved, lp.user_norm2.data(), lp.item_norm2.data());
     return lp;
+  }
+
+  // PrintLosses of the weighted models (safer2.h:337-413, erm_mf.h:303-377,
+  // cvar_mf.h:332-406 -- identical): loss = sum of the user losses, the
+  // regularisers with UserRegularizationValue / ItemRegularizationValue.
+  void PrintWeightedLosses(const Dataset& data, float reg, float w, float alpha) {
+    if (!print_trainstats_) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    const LossParts lp = ComputeLossParts(data);
+    const Csr& uc = data.user_csr();
+    const Csr& ic = data.item_csr();
+    float loss_reg = 0.0f, reg_user_now = 0.0f, reg_item_now = 0.0f;
+    for (int64_t u = 0; u < uc.rows(); ++u) {
+      if (!uc.len(u)) continue;
+      const float n2 = lp.user_norm2[u];
+      loss_reg += n2 * (reg * (1 + w * num_items_));
+      reg_user_now += n2;
+    }
+    for (int64_t i = 0; i < ic.rows(); ++i) {
+      if (!ic.len(i)) continue;
+      const float n2 = lp.item_norm2[i];
+      loss_reg += n2 * (reg * (item_reg_[i] + alpha * w * num_users_));
+      reg_item_now += n2;
+    }
+    const float loss = user_loss_.sum();
+    const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                        std::chrono::steady_clock::now() - t0)
+                        .count();
+    CheckNaN(loss);
+    LOG(INFO) << format(
+        "Loss={0:.2f} Loss_observed={1:.2f} Loss_unobserved={2:.2f} Loss_reg={3:.2f} "
+        "Loss_reg (user)={4:.2f} Loss_reg (item)={5:.2f}",
+        loss, lp.observed / data.num_tuples(), lp.unobserved / num_items_ / num_users_, loss_reg,
+        reg_user_now / num_users_, reg_item_now / num_items_);
+    LOG(INFO) << format("Time={0}", (int64_t)ms);
   }
 
   static double RowSqNorm(const MatrixXf& M, int64_t r) {

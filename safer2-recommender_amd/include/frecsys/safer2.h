@@ -262,36 +262,7 @@ class SAFER2Recommender : public detail::DeviceModel {
 
   // PrintLosses (safer2.h:337-413), diagnostics only.
   void PrintLosses(const Dataset& data) {
-    if (!print_trainstats_) return;
-    const auto t0 = std::chrono::steady_clock::now();
-    const LossParts lp = ComputeLossParts(data);
-    const MatrixXf U = dev_->Get(DeviceContext::USER), V = dev_->Get(DeviceContext::ITEM);
-    const Csr& uc = data.user_csr();
-    const Csr& ic = data.item_csr();
-    float loss_reg = 0.0f, reg_user_now = 0.0f, reg_item_now = 0.0f;
-    for (int64_t u = 0; u < uc.rows(); ++u) {
-      if (!uc.len(u)) continue;
-      const float n2 = (float)RowSqNorm(U, u);
-      loss_reg += n2 * (regularization_ * (1 + unobserved_weight_ * num_items_));
-      reg_user_now += n2;
-    }
-    for (int64_t i = 0; i < ic.rows(); ++i) {
-      if (!ic.len(i)) continue;
-      const float n2 = (float)RowSqNorm(V, i);
-      loss_reg += n2 * (regularization_ * (item_reg_[i] + alpha_ * unobserved_weight_ * num_users_));
-      reg_item_now += n2;
-    }
-    const float loss = user_loss_.sum();
-    const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(
-                        std::chrono::steady_clock::now() - t0)
-                        .count();
-    CheckNaN(loss);
-    LOG(INFO) << format(
-        "Loss={0:.2f} Loss_observed={1:.2f} Loss_unobserved={2:.2f} Loss_reg={3:.2f} "
-        "Loss_reg (user)={4:.2f} Loss_reg (item)={5:.2f}",
-        loss, lp.observed / data.num_tuples(), lp.unobserved / num_items_ / num_users_, loss_reg,
-        reg_user_now / num_users_, reg_item_now / num_items_);
-    LOG(INFO) << format("Time={0}", (int64_t)ms);
+    PrintWeightedLosses(data, regularization_, unobserved_weight_, alpha_);
   }
 
   quantile::Smoother smoother_;
