@@ -17,6 +17,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
+#include <thread>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -63,18 +65,37 @@ class Dataset {
     const char* q = p;
     while (q < end && *q != '\n') ++q;  // discard header (dataset.h:79-80)
     if (q < end) ++q;
-    while (q < end) {
-      // one "user,item" line; atoi semantics (dataset.h:84-85)
-      const char* ls = q;
-      while (q < end && *q != '\n') ++q;
-      const char* le = q;
-      if (q < end) ++q;
-      if (le > ls && le[-1] == '\r') --le;
-      if (le == ls) continue;
-      const char* comma = ls;
-      while (comma < le && *comma != ',') ++comma;
-      users_.push_back(parse_int(ls, comma));
-      items_.push_back(comma < le ? parse_int(comma + 1, le) : 0);
+    // Parallel parse: the body is cut into chunks at
+    // line boundaries, parsed by one thread each, and concatenated in chunk
+    // order -- the tuples keep file order exactly as a sequential read.
+    const size_t body = (size_t)(end - q);
+    int nt = (int)std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+    if (const char* e = getenv("FRECSYS_LOAD_THREADS")) nt = std::max(1, atoi(e));
+    if (body < ((size_t)1 << 20)) nt = 1;
+    std::vector<const char*> cut((size_t)nt + 1, end);
+    cut[0] = q;
+    for (int t = 1; t < nt; ++t) {
+      const char* c = q + body * t / nt;
+      if (c < cut[t - 1]) c = cut[t - 1];
+      while (c < end && c[-1] != '\n') ++c;  // start of the next line
+      cut[t] = c;
+    }
+    std::vector<std::vector<int32_t>> us((size_t)nt), is((size_t)nt);
+    auto parse = [&](int t) { parse_lines(cut[t], cut[t + 1], &us[t], &is[t]); };
+    if (nt == 1) {
+      parse(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 0; t < nt; ++t) th.emplace_back(parse, t);
+      for (auto& x : th) x.join();
+    }
+    size_t total = 0;
+    for (int t = 0; t < nt; ++t) total += us[t].size();
+    users_.reserve(total);
+    items_.reserve(total);
+    for (int t = 0; t < nt; ++t) {
+      users_.insert(users_.end(), us[t].begin(), us[t].end());
+      items_.insert(items_.end(), is[t].begin(), is[t].end());
     }
     if (p) munmap((void*)p, n);
     close(fd);
@@ -137,6 +158,22 @@ class Dataset {
   // dataset.h:43-61) and unused; it is deliberately not provided.
 
  private:
+  // "user,item" lines of [q, end); atoi semantics (dataset.h:84-85).
+  static void parse_lines(const char* q, const char* end, std::vector<int32_t>* users,
+                          std::vector<int32_t>* items) {
+    while (q < end) {
+      const char* ls = q;
+      while (q < end && *q != '\n') ++q;
+      const char* le = q;
+      if (q < end) ++q;
+      if (le > ls && le[-1] == '\r') --le;
+      if (le == ls) continue;
+      const char* comma = ls;
+      while (comma < le && *comma != ',') ++comma;
+      users->push_back(parse_int(ls, comma));
+      items->push_back(comma < le ? parse_int(comma + 1, le) : 0);
+    }
+  }
   static int32_t parse_int(const char* b, const char* e) {
     while (b < e && (*b == ' ' || *b == '\t')) ++b;
     bool neg = false;
