@@ -16,7 +16,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 CXXFLAGS := -O3 -std=c++17 -Wall -I include -I $(PKG)/include -pthread
 
 HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/dual.hip $(CSRC)/spectral.hip $(CSRC)/gramian.hip \
-            $(CSRC)/loss.hip $(CSRC)/wide.hip $(CSRC)/topk.hip \
+            $(CSRC)/loss.hip $(CSRC)/wide.hip $(CSRC)/topk.hip $(CSRC)/pp.hip \
             $(CSRC)/capi.hip
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h $(CSRC)/chol.h include/frecsys_hip.h

@@ -160,6 +160,24 @@ int frecsys_solve_side(frecsys_ctx* ctx, int32_t side,
  * on device); for USER it is gathered across ranks first. */
 int frecsys_user_loss(frecsys_ctx* ctx, int32_t side, float beta, int32_t half,
                       float* host_out);
+/* ---- iALS++ subspace solver (ialspp.h) ----
+ * Rating index of every CSR entry of side USER or ITEM (the tuple's position
+ * in the training file: the second member of the by_user / by_item pairs),
+ * [nnz of side]; allocates the prediction vector of the training tuples.
+ * EVAL rows use their CSR position as rating index. */
+int frecsys_pp_set_rating_index(frecsys_ctx* ctx, int32_t side, const int32_t* rix);
+/* PredictDataset (ialspp.h:480-520) over the rows of side USER (training
+ * prediction vector) or EVAL (fold-in prediction vector):
+ * pred[rating index] = item . user. */
+int frecsys_pp_predict(frecsys_ctx* ctx, int32_t side);
+/* One block Step + ProjectBlock (ialspp.h:351-424, 85-145) of every row of
+ * `side` (USER, ITEM or EVAL) on columns [start, end), end - start <= 128,
+ * against the other side's embeddings and G[other] (params: reg, reg_exp,
+ * unobserved_weight).  Updates the block of the rows and their predictions.
+ * Every rank runs every row (replicas: the prediction vector is not
+ * sharded).  residual (may be NULL): sum of squared block deltas. */
+int frecsys_pp_step(frecsys_ctx* ctx, int32_t side, int32_t start, int32_t end,
+                    const frecsys_solve_params* params, double* residual);
 /* Fold-in evaluation ranking (replaces the scoring + top-K of
  * EvaluateDatasetInternal / EvaluateUser, recommender.h:78-199): for every
  * row r of the EVAL side, scores s = V u_r over all items (fp32), the items

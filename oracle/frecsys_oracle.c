@@ -527,6 +527,164 @@ int64_t oracle_step(int64_t n_rows, const int64_t* row_ptr, const int32_t* col, 
 }
 
 /* ------------------------------------------------------------------ */
+/* iALS++ (ialspp.h): PredictDataset (:480-520), Step (:351-424) with   */
+/* ProjectBlock (:85-145) on one column block [start, end).            */
+/* ------------------------------------------------------------------ */
+typedef struct {
+  const int64_t* row_ptr;
+  const int32_t* col;
+  const int32_t* rix;
+  const float* X;
+  const float* E;
+  float* Eout;
+  float* pred;
+  const float* Gl;   /* b x b   local Gramian  (:360-361) */
+  const float* Glg;  /* b x dim local-global   (:362-363) */
+  int64_t n_other;
+  int dim, start, b;
+  float reg, reg_exp, w;
+  double* resid; /* per row */
+  atomic_llong first_fail;
+} pp_ctx;
+
+static void pp_predict_row(void* vctx, int64_t r, float* s) {
+  pp_ctx* c = (pp_ctx*)vctx;
+  (void)s;
+  const float* u = c->E + (size_t)r * c->dim;
+  for (int64_t k = c->row_ptr[r]; k < c->row_ptr[r + 1]; ++k) {
+    const float* x = c->X + (size_t)c->col[k] * c->dim;
+    float t = 0.f;
+    for (int j = 0; j < c->dim; ++j) t += x[j] * u[j];
+    c->pred[c->rix[k]] = t;
+  }
+}
+
+void oracle_pp_predict(int64_t n_rows, const int64_t* row_ptr, const int32_t* col,
+                       const int32_t* rix, const float* X, int dim, const float* E, float* pred,
+                       int nthreads) {
+  pp_ctx c;
+  memset(&c, 0, sizeof(c));
+  c.row_ptr = row_ptr;
+  c.col = col;
+  c.rix = rix;
+  c.X = X;
+  c.E = E;
+  c.pred = pred;
+  c.dim = dim;
+  run_pool(pp_predict_row, &c, n_rows, nthreads, 1);
+}
+
+static void pp_step_row(void* vctx, int64_t r, float* s) {
+  pp_ctx* c = (pp_ctx*)vctx;
+  const int64_t h = c->row_ptr[r + 1] - c->row_ptr[r];
+  if (h == 0) return;
+  const int b = c->b, d = c->dim, st = c->start;
+  float *A = s, *T = s + (size_t)b * b, *rhs = T + (size_t)b * b, *nv = rhs + b;
+  const float* u = c->E + (size_t)r * d;
+  const int32_t* hist = c->col + c->row_ptr[r];
+  /* reg = RegularizationValue(h, num_items) (:377, :313-318) */
+  const float reg = c->reg * powf((float)h + c->w * (float)c->n_other, c->reg_exp);
+  for (int i = 0; i < b * b; ++i) A[i] = c->w * c->Gl[i];            /* :95 */
+  for (int i = 0; i < b; ++i) A[(size_t)i * b + i] += reg;           /* :97-99 */
+  memset(rhs, 0, sizeof(float) * b);
+  for (int64_t k = 0; k < h; ++k) {                                  /* :107-121 */
+    const float* x = c->X + (size_t)hist[k] * d + st;
+    const float res = c->pred[c->rix[c->row_ptr[r] + k]] - 1.0f;
+    for (int i = 0; i < b; ++i) rhs[i] += x[i] * res;
+  }
+  /* rank updates in 128-column batches (:102-131), lower only */
+  for (int64_t k0 = 0; k0 < h; k0 += KMAXBATCH) {
+    const int64_t cnt = h - k0 < KMAXBATCH ? h - k0 : KMAXBATCH;
+    for (int i = 0; i < b; ++i) memset(T + (size_t)i * b, 0, sizeof(float) * (i + 1));
+    for (int64_t k = k0; k < k0 + cnt; ++k) {
+      const float* x = c->X + (size_t)hist[k] * d + st;
+      for (int i = 0; i < b; ++i)
+        for (int j = 0; j <= i; ++j) T[(size_t)i * b + j] += x[i] * x[j];
+    }
+    add_lower(A, T, b);
+  }
+  for (int i = 0; i < b; ++i) {                                      /* :134-137 */
+    float t = 0.f;
+    for (int j = 0; j < d; ++j) t += c->Glg[(size_t)i * d + j] * u[j];
+    rhs[i] += c->w * t;
+    rhs[i] += reg * u[st + i];
+  }
+  if (cholesky_lower(A, b)) {                                        /* :139-140 */
+    long long cur = atomic_load(&c->first_fail);
+    while ((cur == 0 || cur > r + 1) &&
+           !atomic_compare_exchange_weak(&c->first_fail, &cur, (long long)(r + 1))) {
+    }
+    return;
+  }
+  cholesky_solve(A, b, rhs, nv);
+  double res2 = 0.0;
+  float* out = c->Eout + (size_t)r * d + st;
+  for (int i = 0; i < b; ++i) {
+    const float nw = u[st + i] - nv[i];                              /* :141 */
+    nv[i] = nw - u[st + i];                                          /* delta (:398-399) */
+    out[i] = nw;
+    res2 += (double)nv[i] * nv[i];
+  }
+  for (int64_t k = 0; k < h; ++k) {                                  /* :400-404 */
+    const float* x = c->X + (size_t)hist[k] * d + st;
+    float t = 0.f;
+    for (int i = 0; i < b; ++i) t += nv[i] * x[i];
+    c->pred[c->rix[c->row_ptr[r] + k]] += t;
+  }
+  c->resid[r] = res2;
+}
+
+int64_t oracle_pp_step(int64_t n_rows, const int64_t* row_ptr, const int32_t* col,
+                       const int32_t* rix, const float* X, int64_t n_other, int dim, float* E,
+                       float* pred, int start, int end, float reg, float reg_exp, float w,
+                       double* residual, int nthreads) {
+  const int b = end - start;
+  pp_ctx c;
+  memset(&c, 0, sizeof(c));
+  float* Gl = (float*)calloc((size_t)b * b, sizeof(float));
+  float* Glg = (float*)calloc((size_t)b * dim, sizeof(float));
+  float* Ecopy = (float*)malloc(sizeof(float) * (size_t)(n_rows > 0 ? n_rows : 1) * dim);
+  double* res = (double*)calloc((size_t)(n_rows > 0 ? n_rows : 1), sizeof(double));
+  /* local_gramian = Xb^T Xb, local_global = Xb^T X (:356-363) */
+  for (int64_t o = 0; o < n_other; ++o) {
+    const float* x = X + (size_t)o * dim;
+    for (int i = 0; i < b; ++i) {
+      const float a = x[start + i];
+      for (int j = 0; j < b; ++j) Gl[(size_t)i * b + j] += a * x[start + j];
+      for (int j = 0; j < dim; ++j) Glg[(size_t)i * dim + j] += a * x[j];
+    }
+  }
+  memcpy(Ecopy, E, sizeof(float) * (size_t)n_rows * dim);
+  c.row_ptr = row_ptr;
+  c.col = col;
+  c.rix = rix;
+  c.X = X;
+  c.E = Ecopy;
+  c.Eout = E;
+  c.pred = pred;
+  c.Gl = Gl;
+  c.Glg = Glg;
+  c.n_other = n_other;
+  c.dim = dim;
+  c.start = start;
+  c.b = b;
+  c.reg = reg;
+  c.reg_exp = reg_exp;
+  c.w = w;
+  c.resid = res;
+  atomic_init(&c.first_fail, 0);
+  run_pool(pp_step_row, &c, n_rows, nthreads, (size_t)2 * b * b + 2 * b);
+  double tot = 0.0;
+  for (int64_t r = 0; r < n_rows; ++r) tot += res[r];
+  if (residual) *residual = tot;
+  free(Gl);
+  free(Glg);
+  free(Ecopy);
+  free(res);
+  return (int64_t)atomic_load(&c.first_fail);
+}
+
+/* ------------------------------------------------------------------ */
 /* User loss: ComputeLoss ials.h:70-86 / safer2.h:85-101 via           */
 /* ComputeUserLoss ials.h:367-408 / safer2.h:558-596.                  */
 /* ------------------------------------------------------------------ */

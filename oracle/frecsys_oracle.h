@@ -102,6 +102,16 @@ int64_t oracle_step(int64_t n_rows, const int64_t* row_ptr,
 
 /* ---- user loss (ials.h:70-86 with half=0; safer2.h:85-101 half=1) ----
  * Rows with no history get loss 0 (never written in the reference). */
+/* iALS++ (ialspp.h): PredictDataset (pred[rix[k]] = X[col[k]] . E[row]) and one
+ * block Step + ProjectBlock of a side on columns [start, end); E updated in
+ * place, pred updated with each row's delta.  Returns first failing row + 1. */
+void oracle_pp_predict(int64_t n_rows, const int64_t* row_ptr, const int32_t* col,
+                       const int32_t* rix, const float* X, int dim, const float* E, float* pred,
+                       int nthreads);
+int64_t oracle_pp_step(int64_t n_rows, const int64_t* row_ptr, const int32_t* col,
+                       const int32_t* rix, const float* X, int64_t n_other, int dim, float* E,
+                       float* pred, int start, int end, float reg, float reg_exp, float w,
+                       double* residual, int nthreads);
 void oracle_user_loss(int64_t n_users, const int64_t* row_ptr,
                       const int32_t* col, const float* U, const float* V,
                       int dim, const float* G, float beta, int half,

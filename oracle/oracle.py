@@ -60,6 +60,9 @@ def lib():
             "oracle_model_fold_in": (I64, [P, I64, P, P, P]),
             "oracle_evaluate": (None, [I64, P, P, I64, ctypes.c_int, P, P, P, P, P, ctypes.c_int,
                                        P, P, ctypes.c_int]),
+            "oracle_pp_predict": (None, [I64, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int]),
+            "oracle_pp_step": (I64, [I64, P, P, P, P, I64, ctypes.c_int, P, P, ctypes.c_int,
+                                     ctypes.c_int, F, F, F, P, ctypes.c_int]),
             "oracle_mt_seed": (None, [P, ctypes.c_uint32]),
             "oracle_mt_next": (ctypes.c_uint32, [P]),
         }
@@ -113,6 +116,32 @@ def step(row_ptr, col, X, G, kind, reg, w, reg_exp=1.0, alpha=0.0, stepsize=0.0,
     rc = lib().oracle_step(n, _p(rp), _p(cl), _p(X), X.shape[0], d, _p(G), ctypes.byref(sp),
                            _p(Ev), _p(out), nthreads)
     return out, int(rc)
+
+
+def pp_predict(row_ptr, col, rix, X, E, pred, nthreads=0):
+    """iALS++ PredictDataset into pred (float32, in place)."""
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    cl = np.ascontiguousarray(col, np.int32)
+    rx = np.ascontiguousarray(rix, np.int32)
+    X, E = f32(X), f32(E)
+    assert pred.dtype == np.float32 and pred.flags.c_contiguous
+    lib().oracle_pp_predict(len(rp) - 1, _p(rp), _p(cl), _p(rx), _p(X), X.shape[1], _p(E),
+                            _p(pred), nthreads)
+
+
+def pp_step(row_ptr, col, rix, X, E, pred, start, end, reg, w, reg_exp=1.0, nthreads=0):
+    """iALS++ block Step on columns [start, end): E (float32) and pred updated
+    in place.  Returns (first failing row + 1 or 0, residual)."""
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    cl = np.ascontiguousarray(col, np.int32)
+    rx = np.ascontiguousarray(rix, np.int32)
+    X = f32(X)
+    assert E.dtype == np.float32 and E.flags.c_contiguous
+    res = ctypes.c_double(0.0)
+    rc = lib().oracle_pp_step(len(rp) - 1, _p(rp), _p(cl), _p(rx), _p(X), X.shape[0], X.shape[1],
+                              _p(E), _p(pred), start, end, reg, reg_exp, w, ctypes.byref(res),
+                              nthreads)
+    return int(rc), res.value
 
 
 def user_loss(row_ptr, col, U, V, G, beta, half, nthreads=0):

@@ -99,6 +99,11 @@ struct frecsys_ctx {
   // wide dims (Dp = 512 / 1024): tridiagonalisation work, d-space workspace
   float* tri_work = nullptr;
   size_t cap_tri_work = 0;
+  int32_t* d_rix[2] = {nullptr, nullptr};  // iALS++: rating index per CSR entry
+  float* d_pred[2] = {nullptr, nullptr};   // iALS++: training / EVAL prediction vectors
+  size_t cap_pred[2] = {0, 0};
+  float* d_resid = nullptr;
+  size_t cap_resid = 0;
   float* d_rows = nullptr;       // train stats: per-row values
   size_t cap_rows = 0;
   float* d_gstat = nullptr;      // train stats: U^T U, V^T V
@@ -564,6 +569,11 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (c->wide_ws) (void)hipFree(c->wide_ws);
   if (c->d_scores) (void)hipFree(c->d_scores);
   if (c->d_rows) (void)hipFree(c->d_rows);
+  for (int s = 0; s < 2; ++s) {
+    if (c->d_rix[s]) (void)hipFree(c->d_rix[s]);
+    if (c->d_pred[s]) (void)hipFree(c->d_pred[s]);
+  }
+  if (c->d_resid) (void)hipFree(c->d_resid);
   if (c->d_gstat) (void)hipFree(c->d_gstat);
   if (c->d_dot) (void)hipFree(c->d_dot);
   if (c->d_topk) (void)hipFree(c->d_topk);
@@ -1137,6 +1147,117 @@ int frecsys_eval_topk(frecsys_ctx* c, int32_t k, int32_t* topk) {
   HIP_TRY(c, hipMemcpyAsync(topk, c->d_topk, sizeof(int32_t) * n * k, hipMemcpyDeviceToHost,
                             c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_pp_set_rating_index(frecsys_ctx* c, int32_t side, const int32_t* rix) {
+  if (!c || (side != 0 && side != 1) || !rix)
+    return fail(c, FRECSYS_ERR_INVALID, "pp_set_rating_index: bad arguments");
+  if (!c->rp[side]) return fail(c, FRECSYS_ERR_INVALID, "pp_set_rating_index: no CSR");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int64_t nnz = c->nnz[side];
+  for (int64_t k = 0; k < nnz; ++k)
+    if (rix[k] < 0 || rix[k] >= nnz)
+      return fail(c, FRECSYS_ERR_INVALID, "pp_set_rating_index: index out of range");
+  if (c->d_rix[side]) HIP_TRY(c, hipFree(c->d_rix[side]));
+  c->d_rix[side] = nullptr;
+  HIP_TRY(c, hipMalloc((void**)&c->d_rix[side], sizeof(int32_t) * std::max<int64_t>(nnz, 1)));
+  if (nnz)
+    HIP_TRY(c, hipMemcpy(c->d_rix[side], rix, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
+  return ensure(c, &c->d_pred[0], &c->cap_pred[0], (size_t)std::max<int64_t>(nnz, 1));
+}
+
+namespace {
+PPArgs pp_args(frecsys_ctx* c, int side) {
+  const int other = side == 1 ? 0 : 1;
+  PPArgs a{};
+  a.col = c->col[side];
+  a.rix = side == 2 ? nullptr : c->d_rix[side];
+  a.pred = c->d_pred[side == 2 ? 1 : 0];
+  a.X = c->emb[other];
+  a.G = c->gram[other];
+  a.E = c->emb[side];
+  a.Dp = c->Dp;
+  a.n_other = c->n[other];
+  a.fail = c->d_fail;
+  return a;
+}
+}  // namespace
+
+int frecsys_pp_predict(frecsys_ctx* c, int32_t side) {
+  if (!c || (side != 0 && side != 2)) return fail(c, FRECSYS_ERR_INVALID, "pp_predict: bad side");
+  if (!c->rp[side]) return fail(c, FRECSYS_ERR_INVALID, "pp_predict: no CSR");
+  if (side == 0 && !c->d_rix[0])
+    return fail(c, FRECSYS_ERR_INVALID, "pp_predict: no rating index (pp_set_rating_index)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (side == 2) {
+    int rc = ensure(c, &c->d_pred[1], &c->cap_pred[1], (size_t)std::max<int64_t>(c->nnz[2], 1));
+    if (rc) return rc;
+  }
+  PPArgs a = pp_args(c, side);
+  HIP_TRY(c, launch_pp_predict(a, c->rp[side], c->n[side], c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
+                    const frecsys_solve_params* p, double* residual) {
+  if (!c || !valid_side(side) || !p) return fail(c, FRECSYS_ERR_INVALID, "pp_step: bad arguments");
+  if (start < 0 || end > c->dim || end - start < 1 || end - start > 128)
+    return fail(c, FRECSYS_ERR_INVALID, "pp_step: block must satisfy 0 <= start < end <= dim, "
+                                        "end - start <= 128");
+  if (!c->rp[side]) return fail(c, FRECSYS_ERR_INVALID, "pp_step: no CSR");
+  if (side != 2 && !c->d_rix[side])
+    return fail(c, FRECSYS_ERR_INVALID, "pp_step: no rating index (pp_set_rating_index)");
+  if (!c->d_pred[side == 2 ? 1 : 0])
+    return fail(c, FRECSYS_ERR_INVALID, "pp_step: no prediction vector (pp_predict)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  // every rank runs every row: the work queue of the whole side
+  const int64_t lo = 0, hi = c->n[side];
+  std::vector<QueueRec> recs((size_t)(hi - lo));
+  const std::vector<int64_t>& rp = side == 2 ? c->host_rp_eval : c->host_rp[side];
+  for (int64_t i = lo; i < hi; ++i) recs[i - lo] = QueueRec{(int32_t)i, (int32_t)(rp[i + 1] - rp[i]), rp[i]};
+  std::stable_sort(recs.begin(), recs.end(),
+                   [](const QueueRec& x, const QueueRec& y) { return x.h > y.h; });
+  QueueRec* d_q = nullptr;
+  HIP_TRY(c, hipMalloc((void**)&d_q, sizeof(QueueRec) * std::max<size_t>(recs.size(), 1)));
+  HIP_TRY(c, hipMemcpyAsync(d_q, recs.data(), sizeof(QueueRec) * recs.size(), hipMemcpyHostToDevice,
+                            c->stream));
+  int rc = ensure(c, &c->d_resid, &c->cap_resid, std::max<size_t>(recs.size(), 1));
+  if (rc) return rc;
+  PPArgs a = pp_args(c, side);
+  a.order = d_q;
+  a.n_rows = (int64_t)recs.size();
+  a.start = start;
+  a.bw = end - start;
+  a.reg = p->reg;
+  a.reg_exp = p->reg_exp;
+  a.w = p->unobserved_weight;
+  a.resid = c->d_resid;
+  const unsigned long long none = ~0ull;
+  HIP_TRY(c, hipMemcpyAsync(c->d_fail, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
+  {
+    ScopedTimer t(c, "pp_step");
+    HIP_TRY(c, launch_pp_step(a, c->stream));
+    t.stop();
+  }
+  std::vector<float> res(recs.size());
+  unsigned long long f = none;
+  HIP_TRY(c, hipMemcpyAsync(&f, c->d_fail, sizeof(f), hipMemcpyDeviceToHost, c->stream));
+  if (residual && !recs.empty())
+    HIP_TRY(c, hipMemcpyAsync(res.data(), c->d_resid, sizeof(float) * recs.size(),
+                              hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipFree(d_q));
+  if (f != none) {
+    c->err_entity = (int64_t)(f - 1);
+    return fail(c, FRECSYS_ERR_NOT_SPD, "pp_step: block matrix not SPD");
+  }
+  if (residual) {
+    double s = 0.0;
+    for (float v : res) s += (double)v;  // zero rows (empty histories) stay 0
+    *residual = s;
+  }
   return FRECSYS_OK;
 }
 

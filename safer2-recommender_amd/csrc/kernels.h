@@ -156,6 +156,27 @@ __host__ __device__ inline int64_t blk_t(int64_t p, int j, int k, int Dp) {
 }
 hipError_t launch_gramian(int Dp, const GramArgs& a, hipStream_t s);
 
+// iALS++ block step (pp.hip; ialspp.h:85-145, 351-424).
+struct PPArgs {
+  const QueueRec* order;    // entities of the launch (LPT order)
+  int64_t n_rows;
+  const int32_t* col;       // CSR columns of the solved side
+  const int32_t* rix;       // rating index per CSR entry (nullptr: the CSR position)
+  float* pred;              // prediction vector, by rating index
+  const float* X;           // other side, ld Dp
+  const float* G;           // Gramian of the other side, Dp x Dp
+  float* E;                 // solved side, ld Dp (block updated in place)
+  int Dp, start, bw;        // block columns [start, start + bw), bw <= 128
+  float reg, reg_exp, w;
+  int64_t n_other;
+  float* resid;             // [n_rows] squared delta norms, or nullptr
+  unsigned long long* fail;
+};
+hipError_t launch_pp_step(const PPArgs& a, hipStream_t s);
+// PredictDataset over the CSR rows 0..n_rows-1 (E = the rows' embeddings).
+hipError_t launch_pp_predict(const PPArgs& a, const int64_t* row_ptr, int64_t n_rows,
+                             hipStream_t s);
+
 // Fold-in scoring + top-k (topk.hip): rows r0..r0+n-1 of X against the m
 // rows of Y; S: [n][m] workspace; out: [n][k].
 hipError_t launch_eval_topk(const float* X, int64_t r0, int64_t n, const float* Y, int64_t m,

@@ -1,0 +1,202 @@
+// pp.hip -- iALS++ subspace block step on gfx950 (SURVEY 8(f) rank 2;
+// reference ialspp.h: Step :351-424 with ProjectBlock :85-145, and
+// PredictDataset :480-520).
+//
+// Per block of columns [s, s+bw) (bw = block_size <= 128) and per entity
+// (one workgroup each, LPT queue order):
+//   A = w*G[s:e, s:e] + lam*I + sum_j x_j,b x_j,b^T     (bw x bw, MFMA SYRK)
+//   r = sum_j x_j,b (pred_j - 1) + w*G[s:e, :] u + lam*u_b
+//   u_b <- u_b - A^-1 r                                 (chol_solve_tiles)
+//   pred_j += (u_b' - u_b) . x_j,b                      (the entity's own ratings)
+// The block is padded to 32-column tiles (identity on the padded diagonal).
+// pred is the device-resident prediction vector indexed by rating index
+// (position of the tuple in the training file); each rating belongs to one
+// entity per side, so the per-entity updates never race.
+#include <hip/hip_runtime.h>
+
+#include "chol.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace frecsys_hip {
+
+namespace {
+
+template <int TB>
+struct PPCfg {
+  static constexpr int BWP = 32 * TB;               // padded block width
+  static constexpr int NT = TB * (TB + 1) / 2;
+  static constexpr int MT = (NT + 3) / 4;           // tiles per wave (4 waves)
+  static constexpr int TILES = NT * 1024;
+  static constexpr int STAGE = 32 * BWP;
+};
+
+template <int TB>
+__global__ void __launch_bounds__(256) pp_block_kernel(PPArgs a) {
+  using C = PPCfg<TB>;
+  constexpr int BWP = C::BWP, NT = C::NT, MT = C::MT;
+  __shared__ __attribute__((aligned(16))) float tiles[C::TILES];
+  __shared__ float stage[C::STAGE];
+  __shared__ float us[1024];
+  __shared__ int ids[32];
+  __shared__ float coef[32];
+  __shared__ float bvec[BWP], xvec[BWP];
+  __shared__ float part[4 * 32];
+  __shared__ float red[4];
+  __shared__ int flag[1];
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const QueueRec rec = a.order[blockIdx.x];
+  const int64_t e = rec.entity, h = rec.h, p0 = rec.p0;
+  if (h == 0) return;
+  const int Dp = a.Dp, s0 = a.start, bw = a.bw;
+  // RegularizationValue(h, num_items) (ialspp.h:377, 313-318)
+  const float lam = a.reg * powf((float)h + a.w * (float)a.n_other, a.reg_exp);
+  for (int c = tid; c < Dp; c += 256) us[c] = a.E[e * Dp + c];
+  if (tid == 0) flag[0] = 0;
+
+  f32x16 acc[MT];
+  int aoff[MT], boff[MT];
+  bool valid[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int t = wave + 4 * m;
+    valid[m] = t < NT;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= t) ++I;
+    const int J = t - I * (I + 1) / 2;
+    aoff[m] = 32 * I + lo;
+    boff[m] = 32 * J + lo;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int gi = 32 * I + acc_row(q, hi), gj = 32 * J + lo;
+      float v = 0.0f;
+      if (valid[m]) {
+        if (gi < bw && gj < bw)
+          v = a.w * a.G[(int64_t)(s0 + gi) * Dp + s0 + gj] + (gi == gj ? lam : 0.0f);
+        else if (gi == gj)
+          v = 1.0f;  // padded coordinate: identity
+      }
+      acc[m][q] = v;
+    }
+  }
+  float bacc = 0.0f;
+  for (int64_t k0 = 0; k0 < h; k0 += 32) {
+    __syncthreads();
+    if (tid < 32) {
+      const int64_t k = k0 + tid;
+      ids[tid] = k < h ? a.col[p0 + k] : -1;
+      coef[tid] = k < h ? a.pred[a.rix ? a.rix[p0 + k] : p0 + k] - 1.0f : 0.0f;
+    }
+    __syncthreads();
+    for (int i = tid; i < C::STAGE; i += 256) {
+      const int r = i / BWP, cc = i % BWP;
+      const int id = ids[r];
+      stage[i] = (id >= 0 && cc < bw) ? a.X[(int64_t)id * Dp + s0 + cc] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (valid[m]) {
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+          const float* rowp = stage + (2 * s2 + hi) * BWP;
+          acc[m] = mfma32(rowp[aoff[m]], rowp[boff[m]], acc[m]);
+        }
+      }
+    }
+    if (tid < bw) {
+#pragma unroll 8
+      for (int r = 0; r < 32; ++r) bacc += coef[r] * stage[r * BWP + tid];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    if (valid[m]) {
+      const int I = (aoff[m] - lo) >> 5, J = (boff[m] - lo) >> 5;
+      float* tile = tiles + tidx(I, J) * 1024;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) tile[sw(acc_row(q, hi), lo)] = acc[m][q];
+    }
+  }
+  if (tid < BWP) {
+    float r = 0.0f;
+    if (tid < bw) {
+      const float* g = a.G + (int64_t)(s0 + tid) * Dp;
+      float t = 0.0f;
+      for (int c = 0; c < Dp; ++c) t += g[c] * us[c];
+      r = bacc + a.w * t + lam * us[s0 + tid];  // ialspp.h:134-137
+    }
+    bvec[tid] = r;
+  }
+  __syncthreads();
+  chol_solve_tiles<TB, 4>(tiles, bvec, xvec, part, flag, tid, 0);
+  // new block (ialspp.h:141), residual, and the entity's predictions
+  float d2 = 0.0f;
+  if (tid < bw) {
+    const float nw = us[s0 + tid] - xvec[tid];
+    const float dl = nw - us[s0 + tid];
+    xvec[tid] = dl;  // own element only
+    a.E[e * Dp + s0 + tid] = nw;
+    d2 = dl * dl;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);
+  if (lane == 0) red[wave] = d2;
+  __syncthreads();
+  if (tid == 0 && a.resid) a.resid[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  for (int64_t k = wave; k < h; k += 4) {  // ialspp.h:400-404
+    const int id = a.col[p0 + k];
+    float t = 0.0f;
+    for (int c = lane; c < bw; c += 64) t += xvec[c] * a.X[(int64_t)id * Dp + s0 + c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (lane == 0) a.pred[a.rix ? a.rix[p0 + k] : p0 + k] += t;
+  }
+  if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
+}
+
+// pred[rix[k]] = X[col[k]] . E[row], one wave per row (PredictDataset).
+__global__ void __launch_bounds__(256) pp_predict_kernel(PPArgs a, const int64_t* row_ptr,
+                                                         int64_t n_rows) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n_rows) return;
+  const int Dp = a.Dp;
+  const float* u = a.E + r * Dp;
+  for (int64_t k = row_ptr[r]; k < row_ptr[r + 1]; ++k) {
+    const float* x = a.X + (int64_t)a.col[k] * Dp;
+    float t = 0.0f;
+    for (int c = lane; c < Dp; c += 64) t += x[c] * u[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (lane == 0) a.pred[a.rix ? a.rix[k] : k] = t;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_pp_step(const PPArgs& a, hipStream_t s) {
+  if (a.n_rows <= 0) return hipSuccess;
+  if (a.bw < 1 || a.bw > 128 || a.Dp > 1024) return hipErrorInvalidValue;
+  const int tb = (a.bw + 31) / 32;
+  const dim3 g((unsigned)a.n_rows), b(256);
+  switch (tb) {
+    case 1: hipLaunchKernelGGL(pp_block_kernel<1>, g, b, 0, s, a); break;
+    case 2: hipLaunchKernelGGL(pp_block_kernel<2>, g, b, 0, s, a); break;
+    case 3: hipLaunchKernelGGL(pp_block_kernel<3>, g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL(pp_block_kernel<4>, g, b, 0, s, a); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_pp_predict(const PPArgs& a, const int64_t* row_ptr, int64_t n_rows,
+                             hipStream_t s) {
+  if (n_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pp_predict_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, s, a,
+                     row_ptr, n_rows);
+  return hipGetLastError();
+}
+
+}  // namespace frecsys_hip

@@ -34,7 +34,8 @@ EXPORTS = (
     "frecsys_get_embeddings", "frecsys_init_embeddings", "frecsys_snapshot",
     "frecsys_gramian", "frecsys_set_gramian", "frecsys_solve_side", "frecsys_user_loss",
     "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset", "frecsys_debug_basis",
-    "frecsys_eval_topk", "frecsys_train_stats",
+    "frecsys_eval_topk", "frecsys_train_stats", "frecsys_pp_set_rating_index",
+    "frecsys_pp_predict", "frecsys_pp_step",
 )
 
 
@@ -98,6 +99,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_debug_basis": (ctypes.c_int, [P, I32, P, P, P]),
         "frecsys_eval_topk": (ctypes.c_int, [P, I32, P]),
         "frecsys_train_stats": (ctypes.c_int, [P, P, P, P, P]),
+        "frecsys_pp_set_rating_index": (ctypes.c_int, [P, I32, P]),
+        "frecsys_pp_predict": (ctypes.c_int, [P, I32]),
+        "frecsys_pp_step": (ctypes.c_int, [P, I32, I32, I32, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -260,6 +264,21 @@ class Context:
         out = np.zeros((self.n[SIDE_EVAL], k), dtype=np.int32)
         self._check(self.lib.frecsys_eval_topk(self.h, k, _ptr(out)))
         return out
+
+    def pp_set_rating_index(self, side: int, rix: np.ndarray):
+        r = np.ascontiguousarray(rix, dtype=np.int32)
+        self._check(self.lib.frecsys_pp_set_rating_index(self.h, side, _ptr(r)))
+
+    def pp_predict(self, side: int):
+        self._check(self.lib.frecsys_pp_predict(self.h, side))
+
+    def pp_step(self, side: int, start: int, end: int, reg: float, w: float,
+                reg_exp: float = 1.0) -> float:
+        p = _SolveParams(KIND_IALS, reg, reg_exp, w, 0.0, 0.0, 0, 0, None, None, None)
+        res = ctypes.c_double(0.0)
+        self._check(self.lib.frecsys_pp_step(self.h, side, start, end, ctypes.byref(p),
+                                             ctypes.byref(res)))
+        return res.value
 
     def train_stats(self):
         """(observed, unobserved, ||U_r||^2, ||V_r||^2): ComputeLosses' parts."""

@@ -50,6 +50,16 @@ inline Csr build_csr(const std::vector<int32_t>& rows, const std::vector<int32_t
   for (size_t k = 0; k < rows.size(); ++k) c.col[(size_t)fill[rows[k]]++] = cols[k];
   return c;
 }
+// Rating index (tuple position) of every entry of build_csr(rows, ...):
+// the same stable counting sort, storing positions.
+inline std::vector<int32_t> build_rix(const std::vector<int32_t>& rows, int64_t n_rows) {
+  std::vector<int64_t> fill((size_t)n_rows + 1, 0);
+  for (int32_t r : rows) fill[(size_t)r + 1]++;
+  for (int64_t i = 0; i < n_rows; ++i) fill[i + 1] += fill[i];
+  std::vector<int32_t> rix(rows.size());
+  for (size_t k = 0; k < rows.size(); ++k) rix[(size_t)fill[rows[k]]++] = (int32_t)k;
+  return rix;
+}
 }  // namespace detail
 
 class Dataset {
@@ -124,6 +134,11 @@ class Dataset {
     std::call_once(csr_once_[1], [&] { icsr_ = detail::build_csr(items_, users_, max_item_ + 1); });
     return icsr_;
   }
+
+  // Rating index of every CSR entry (the second member of the reference's
+  // by_user / by_item pairs), in CSR order.
+  std::vector<int32_t> user_rix() const { return detail::build_rix(users_, max_user_ + 1); }
+  std::vector<int32_t> item_rix() const { return detail::build_rix(items_, max_item_ + 1); }
 
   // Reference API: SpMatrix with (other id, rating index) pairs.
   const SpMatrix& by_user() const {

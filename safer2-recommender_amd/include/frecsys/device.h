@@ -134,6 +134,32 @@ class DeviceContext {
     if (side != EVAL) bump(side);
   }
 
+  // ---- iALS++ (ialspp.h) ----
+  void PPLoad(const Dataset& d) {
+    LoadTraining(d);
+    if (pp_loaded_ == &d && pp_tuples_ == d.num_tuples()) return;
+    const std::vector<int32_t> ur = d.user_rix(), ir = d.item_rix();
+    check(frecsys_pp_set_rating_index(ctx_, USER, ur.data()), "pp_set_rating_index(user)");
+    check(frecsys_pp_set_rating_index(ctx_, ITEM, ir.data()), "pp_set_rating_index(item)");
+    pp_loaded_ = &d;
+    pp_tuples_ = d.num_tuples();
+  }
+  void PPPredict(int side) { check(frecsys_pp_predict(ctx_, side), "pp_predict"); }
+  double PPStep(int side, int start, int end, const frecsys_solve_params& p) {
+    double r = 0.0;
+    const int rc = frecsys_pp_step(ctx_, side, start, end, &p, &r);
+    if (rc == FRECSYS_ERR_NOT_SPD)
+      LOG(FATAL) << "LLT failed in ProjectBlock for entity " << frecsys_last_error_entity(ctx_);
+    check(rc, "pp_step");
+    if (side != EVAL) bump(side);
+    return r;
+  }
+  // Zero the EVAL embeddings (the fold-in starts from 0, ialspp.h:155-170).
+  void ZeroEval(int dim) {
+    std::vector<float> z((size_t)n_[EVAL] * dim, 0.0f);
+    if (n_[EVAL]) check(frecsys_set_embeddings(ctx_, EVAL, z.data(), dim), "set_embeddings(eval)");
+  }
+
   // ComputeLosses parts on the GPU (frecsys_train_stats).
   void TrainStats(double* observed, double* unobserved, float* user_norm2, float* item_norm2) {
     check(frecsys_train_stats(ctx_, observed, unobserved, user_norm2, item_norm2), "train_stats");
@@ -200,6 +226,8 @@ class DeviceContext {
   const Dataset* loaded_ = nullptr;
   int loaded_tuples_ = -1;
   uint64_t version_[2] = {1, 1};
+  const Dataset* pp_loaded_ = nullptr;
+  int pp_tuples_ = -1;
   uint64_t gram_key_[2] = {0, 0};
   bool gram_valid_[2] = {false, false};
 };

@@ -67,6 +67,13 @@ class DeviceModel : public Recommender {
     data.compact_users(&ids, &csr);
     dev_->LoadEval(csr);
     dev_->Solve(DeviceContext::EVAL, params);
+    return RankEval(k_list, alpha_list, ids, eval_by_user);
+  }
+
+  // Ranking of the projected EVAL rows (ids = their user ids): GPU scoring +
+  // top-K, Recall / NDCG on host (recommender.h:132-199).
+  EvaluationResult RankEval(const VectorXi& k_list, const VectorXf& alpha_list,
+                            const std::vector<int32_t>& ids, const SpMatrix& eval_by_user) {
     const int max_k = std::min<int>(k_list.maxCoeff(), (int)num_items_);
     const std::vector<int32_t> top = dev_->EvalTopK(max_k);
     std::unordered_map<int, int> user_to_ind;

@@ -9,8 +9,8 @@
 // std::random_device), --device (HIP ordinal), --parity_quirks (0/1,
 // SURVEY App. A.1).  One process per GPU for multi-GPU runs: WORLD_SIZE /
 // RANK / LOCAL_RANK from the environment (torchrun-style), RCCL id through
-// FRECSYS_COMM_FILE.  iALS++ / SAFER2++ (ialspp.h, safer2pp.h) are not part
-// of this build.
+// FRECSYS_COMM_FILE.  iALS++ (ialspp.h) runs on the GPU block-step kernels;
+// SAFER2++ (safer2pp.h) is not part of this build.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -22,6 +22,7 @@
 #include "frecsys/cvar_mf.h"
 #include "frecsys/erm_mf.h"
 #include "frecsys/ials.h"
+#include "frecsys/ialspp.h"
 #include "frecsys/safer2.h"
 
 namespace {
@@ -115,6 +116,10 @@ frecsys::Recommender* get_model(const std::string& name, int num_users, int num_
                                      a.f("--l2_reg_exp"), a.f("--uobs_weight"), a.f("--stdev"),
                                      a.f("--alpha"), a.b("--use_cg"),
                                      a.f("--cg_error_tolerance"), a.i("--cg_max_iterations"), o);
+  } else if (name == "ialspp") {
+    r = new frecsys::IALSppRecommender(a.i("--dim"), num_users, num_items, a.f("--l2_reg"),
+                                       a.f("--l2_reg_exp"), a.f("--uobs_weight"),
+                                       a.f("--stdev"), a.f("--alpha"), a.i("--block_size"), o);
   } else if (name == "safer2") {
     r = new frecsys::SAFER2Recommender(
         a.i("--dim"), num_users, num_items, a.f("--l2_reg"), a.f("--uobs_weight"),
@@ -132,7 +137,7 @@ frecsys::Recommender* get_model(const std::string& name, int num_users, int num_
                                        a.f("--uobs_weight"), a.f("--alpha"), a.f("--stepsize"),
                                        a.f("--stdev"), o);
   } else {
-    LOG(FATAL) << "model " << name << " (iALS++ / SAFER2++) is not part of this build";
+    LOG(FATAL) << "model " << name << " (SAFER2++) is not part of this build";
   }
   r->SetPrintResidualStats(a.b("--print_residual_stats"));
   r->SetPrintVarStats(a.b("--print_var_stats"));

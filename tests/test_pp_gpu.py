@@ -1,0 +1,110 @@
+"""iALS++ block coordinate descent on the GPU (csrc/pp.hip; reference
+ialspp.h: Step :351-424, ProjectBlock :85-145, PredictDataset :480-520)
+against the oracle restatement, one full epoch of user/item block steps from
+identical inputs (1e-4 relative per row, like every other solve), the
+fold-in from zero embeddings, and the reference's own quality gate
+(ialspp_test.cc: d=8, block 4, 10 epochs, NDCG@20 >= 0.2) through run_model.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import ML1M, PKG, rel_rows
+from test_parity_gpu import _ctx
+
+pytestmark = pytest.mark.gpu
+
+fh = pytest.importorskip("frecsys_hip")
+
+TOL_ROW = 1e-4
+
+
+def _rix(uc):
+    """Rating index of the user CSR (tuple order) and the item CSR entries."""
+    return (np.arange(len(uc), dtype=np.int32),
+            np.argsort(np.asarray(uc), kind="stable").astype(np.int32))
+
+
+@pytest.mark.parametrize("dim,bs", [(8, 4), (32, 32), (64, 24), (100, 64), (256, 128)])
+def test_pp_epoch_matches_oracle(quirk_data, dim, bs):
+    nu, ni, up, uc, ip, ic = quirk_data
+    reg, w = 0.003, 0.1
+    ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+    urix, irix = _rix(uc)
+    ctx.pp_set_rating_index(fh.SIDE_USER, urix)
+    ctx.pp_set_rating_index(fh.SIDE_ITEM, irix)
+    ctx.pp_predict(fh.SIDE_USER)
+    pred = np.zeros(len(uc), np.float32)
+    O.pp_predict(up, uc, urix, V, U, pred)
+    Uo, Vo = U.copy(), V.copy()
+    for start in range(0, dim, bs):
+        end = min(start + bs, dim)
+        ctx.gramian(fh.SIDE_ITEM)
+        ru = ctx.pp_step(fh.SIDE_USER, start, end, reg, w)
+        rc, ro = O.pp_step(up, uc, urix, Vo, Uo, pred, start, end, reg, w)
+        assert rc == 0 and abs(ru - ro) <= 1e-3 * ro + 1e-12
+        ctx.gramian(fh.SIDE_USER)
+        ctx.pp_step(fh.SIDE_ITEM, start, end, reg, w)
+        rc, _ = O.pp_step(ip, ic, irix, Uo, Vo, pred, start, end, reg, w)
+        assert rc == 0
+    Ug, Vg = ctx.get_embeddings(fh.SIDE_USER), ctx.get_embeddings(fh.SIDE_ITEM)
+    assert rel_rows(Ug, Uo).max() < TOL_ROW
+    assert rel_rows(Vg, Vo).max() < TOL_ROW
+    np.testing.assert_array_equal(Ug[5], U[5])  # idle user untouched
+    np.testing.assert_array_equal(Vg[9], V[9])
+
+
+@pytest.mark.parametrize("dim,bs", [(32, 8), (64, 64)])
+def test_pp_fold_in_from_zero(ml1m, dim, bs):
+    tr, vt, ve = ml1m
+    nu, ni = tr.max_user + 1, tr.max_item + 1
+    up, uc = tr.by_user()
+    ip, ic = tr.by_item()
+    ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+    ids, ep, ec = vt.compact_users()
+    ctx.load_csr(fh.SIDE_EVAL, ep, ec)
+    ctx.set_embeddings(fh.SIDE_EVAL, np.zeros((len(ep) - 1, dim), np.float32))
+    Ue = np.zeros((len(ep) - 1, dim), np.float32)
+    pred = np.zeros(len(ec), np.float32)
+    rix = np.arange(len(ec), dtype=np.int32)
+    ctx.gramian(fh.SIDE_ITEM)
+    for _ in range(2):
+        ctx.pp_predict(fh.SIDE_EVAL)
+        O.pp_predict(ep, ec, rix, V, Ue, pred)
+        for start in range(0, dim, bs):
+            end = min(start + bs, dim)
+            ctx.pp_step(fh.SIDE_EVAL, start, end, 0.003, 0.1)
+            rc, _ = O.pp_step(ep, ec, rix, V, Ue, pred, start, end, 0.003, 0.1)
+            assert rc == 0
+    assert rel_rows(ctx.get_embeddings(fh.SIDE_EVAL), Ue).max() < TOL_ROW
+
+
+def test_pp_rejects_bad_block(quirk_data):
+    nu, ni, up, uc, ip, ic = quirk_data
+    ctx, U, V = _ctx(256, nu, ni, up, uc, ip, ic)
+    urix, irix = _rix(uc)
+    ctx.pp_set_rating_index(fh.SIDE_USER, urix)
+    ctx.pp_predict(fh.SIDE_USER)
+    for s, e in ((0, 0), (0, 129), (250, 257)):
+        with pytest.raises(fh.FrecsysError) as ei:
+            ctx.pp_step(fh.SIDE_USER, s, e, 0.003, 0.1)
+        assert ei.value.code == fh.ERR_INVALID
+
+
+def test_gate_ialspp_run_model():  # ialspp_test.cc:14-80
+    cmd = [os.path.join(PKG, "bin", "run_model"), "--train_data", os.path.join(ML1M, "train.csv"),
+           "--test_train_data", os.path.join(ML1M, "validation_tr.csv"),
+           "--test_test_data", os.path.join(ML1M, "validation_te.csv"), "--seed", "1",
+           "--model_name", "ialspp", "--dim", "8", "--block_size", "4", "--uobs_weight", "0.1",
+           "--l2_reg", "0.003", "--epoch", "10", "--print_train_stats", "1",
+           "--print_residual_stats", "1", "--print_var_stats", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    tail = r.stderr[r.stderr.rindex("Validation Results"):]
+    m = re.search(r"Mean NDCG@20=([0-9.]+)", tail)
+    assert m and float(m.group(1)) >= 0.2, tail[-2000:]
+    assert len(re.findall(r"U residual: [0-9.e+-]+, V residual", r.stderr)) == 10
