@@ -170,10 +170,14 @@ int frecsys_pp_set_rating_index(frecsys_ctx* ctx, int32_t side, const int32_t* r
  * prediction vector) or EVAL (fold-in prediction vector):
  * pred[rating index] = item . user. */
 int frecsys_pp_predict(frecsys_ctx* ctx, int32_t side);
-/* One block Step + ProjectBlock (ialspp.h:351-424, 85-145) of every row of
- * `side` (USER, ITEM or EVAL) on columns [start, end), end - start <= 128,
- * against the other side's embeddings and G[other] (params: reg, reg_exp,
- * unobserved_weight).  Updates the block of the rows and their predictions.
+/* One block Step of every row of `side` (USER, ITEM or EVAL) on columns
+ * [start, end), end - start <= 128, against the other side's embeddings and
+ * G[other]: params->kind IALS = iALS++ Step + ProjectBlock
+ * (ialspp.h:351-424, 85-145; reg, reg_exp, unobserved_weight),
+ * WEIGHTED_U / WEIGHTED_V = SAFER2++ StepU + ProjectU / StepV + ProjectV
+ * (safer2pp.h:449-653, 97-216; entity_weight / entity_reg + other_weight +
+ * alpha as for frecsys_solve_side, G[other] the omega-weighted Gramian for
+ * WEIGHTED_V).  Updates the block of the rows and their predictions.
  * Every rank runs every row (replicas: the prediction vector is not
  * sharded).  residual (may be NULL): sum of squared block deltas. */
 int frecsys_pp_step(frecsys_ctx* ctx, int32_t side, int32_t start, int32_t end,

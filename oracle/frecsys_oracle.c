@@ -541,8 +541,9 @@ typedef struct {
   const float* Gl;   /* b x b   local Gramian  (:360-361) */
   const float* Glg;  /* b x dim local-global   (:362-363) */
   int64_t n_other;
-  int dim, start, b;
-  float reg, reg_exp, w;
+  int dim, start, b, kind;
+  float reg, reg_exp, w, alpha;
+  const float *entity_weight, *entity_reg, *other_weight;
   double* resid; /* per row */
   atomic_llong first_fail;
 } pp_ctx;
@@ -582,15 +583,35 @@ static void pp_step_row(void* vctx, int64_t r, float* s) {
   float *A = s, *T = s + (size_t)b * b, *rhs = T + (size_t)b * b, *nv = rhs + b;
   const float* u = c->E + (size_t)r * d;
   const int32_t* hist = c->col + c->row_ptr[r];
-  /* reg = RegularizationValue(h, num_items) (:377, :313-318) */
-  const float reg = c->reg * powf((float)h + c->w * (float)c->n_other, c->reg_exp);
-  for (int i = 0; i < b * b; ++i) A[i] = c->w * c->Gl[i];            /* :95 */
-  for (int i = 0; i < b; ++i) A[(size_t)i * b + i] += reg;           /* :97-99 */
+  /* kind 0: iALS++ ProjectBlock (ialspp.h:85-145), reg =
+   * RegularizationValue(h, num_items) (:377, :313-318);
+   * kind 1: SAFER2++ ProjectU (safer2pp.h:97-160), reg =
+   * UserRegularizationValue, weight = dual weight;
+   * kind 2: SAFER2++ ProjectV (safer2pp.h:162-216), reg =
+   * ItemRegularizationValue, per-row weight nu_u = omega_u / |H_u|, the
+   * Gramians weighted by omega (StepV, safer2pp.h:530-541). */
+  float reg, wt = 1.0f;
+  if (c->kind == 0) {
+    reg = c->reg * powf((float)h + c->w * (float)c->n_other, c->reg_exp);
+  } else if (c->kind == 1) {
+    reg = c->reg * (1 + c->w * (float)c->n_other);
+    wt = c->entity_weight ? c->entity_weight[r] : 1.0f;
+  } else {
+    reg = c->reg * (c->entity_reg[r] + c->alpha * c->w * (float)c->n_other);
+  }
+  if (c->kind == 1) {
+    memset(A, 0, sizeof(float) * (size_t)b * b);
+  } else {
+    for (int i = 0; i < b * b; ++i) A[i] = c->w * c->Gl[i];          /* :95 / :173 */
+    for (int i = 0; i < b; ++i) A[(size_t)i * b + i] += reg;         /* :97-99 */
+  }
   memset(rhs, 0, sizeof(float) * b);
   for (int64_t k = 0; k < h; ++k) {                                  /* :107-121 */
-    const float* x = c->X + (size_t)hist[k] * d + st;
+    const int32_t o = hist[k];
+    const float* x = c->X + (size_t)o * d + st;
+    const float nu = c->kind == 2 ? c->other_weight[o] : 1.0f;
     const float res = c->pred[c->rix[c->row_ptr[r] + k]] - 1.0f;
-    for (int i = 0; i < b; ++i) rhs[i] += x[i] * res;
+    for (int i = 0; i < b; ++i) rhs[i] += c->kind == 2 ? x[i] * res * nu : x[i] * res;
   }
   /* rank updates in 128-column batches (:102-131), lower only */
   for (int64_t k0 = 0; k0 < h; k0 += KMAXBATCH) {
@@ -598,17 +619,29 @@ static void pp_step_row(void* vctx, int64_t r, float* s) {
     for (int i = 0; i < b; ++i) memset(T + (size_t)i * b, 0, sizeof(float) * (i + 1));
     for (int64_t k = k0; k < k0 + cnt; ++k) {
       const float* x = c->X + (size_t)hist[k] * d + st;
+      const float sq = c->kind == 2 ? sqrtf(c->other_weight[hist[k]]) : 1.0f;
       for (int i = 0; i < b; ++i)
-        for (int j = 0; j <= i; ++j) T[(size_t)i * b + j] += x[i] * x[j];
+        for (int j = 0; j <= i; ++j) T[(size_t)i * b + j] += (x[i] * sq) * (x[j] * sq);
     }
     add_lower(A, T, b);
+  }
+  if (c->kind == 1) { /* safer2pp.h:136-150 */
+    for (int i = 0; i < b; ++i)
+      for (int j = 0; j <= i; ++j) {
+        float v = A[(size_t)i * b + j] / (float)h;
+        v += c->w * c->Gl[(size_t)i * b + j];
+        A[(size_t)i * b + j] = v * wt;
+      }
+    for (int i = 0; i < b; ++i) rhs[i] *= wt / (float)h;
   }
   for (int i = 0; i < b; ++i) {                                      /* :134-137 */
     float t = 0.f;
     for (int j = 0; j < d; ++j) t += c->Glg[(size_t)i * d + j] * u[j];
-    rhs[i] += c->w * t;
+    rhs[i] += c->kind == 1 ? c->w * t * wt : c->w * t;
     rhs[i] += reg * u[st + i];
   }
+  if (c->kind == 1)
+    for (int i = 0; i < b; ++i) A[(size_t)i * b + i] += reg;
   if (cholesky_lower(A, b)) {                                        /* :139-140 */
     long long cur = atomic_load(&c->first_fail);
     while ((cur == 0 || cur > r + 1) &&
@@ -636,8 +669,8 @@ static void pp_step_row(void* vctx, int64_t r, float* s) {
 
 int64_t oracle_pp_step(int64_t n_rows, const int64_t* row_ptr, const int32_t* col,
                        const int32_t* rix, const float* X, int64_t n_other, int dim, float* E,
-                       float* pred, int start, int end, float reg, float reg_exp, float w,
-                       double* residual, int nthreads) {
+                       float* pred, int start, int end, const oracle_solve_params* p,
+                       const float* gram_w, double* residual, int nthreads) {
   const int b = end - start;
   pp_ctx c;
   memset(&c, 0, sizeof(c));
@@ -645,11 +678,13 @@ int64_t oracle_pp_step(int64_t n_rows, const int64_t* row_ptr, const int32_t* co
   float* Glg = (float*)calloc((size_t)b * dim, sizeof(float));
   float* Ecopy = (float*)malloc(sizeof(float) * (size_t)(n_rows > 0 ? n_rows : 1) * dim);
   double* res = (double*)calloc((size_t)(n_rows > 0 ? n_rows : 1), sizeof(double));
-  /* local_gramian = Xb^T Xb, local_global = Xb^T X (:356-363) */
+  /* local_gramian = Xb^T Xb, local_global = Xb^T X (:356-363); weighted
+   * by gram_w (the dual weights) for the SAFER2++ V step */
   for (int64_t o = 0; o < n_other; ++o) {
     const float* x = X + (size_t)o * dim;
+    const float gw = gram_w ? gram_w[o] : 1.0f;
     for (int i = 0; i < b; ++i) {
-      const float a = x[start + i];
+      const float a = gram_w ? x[start + i] * gw : x[start + i];
       for (int j = 0; j < b; ++j) Gl[(size_t)i * b + j] += a * x[start + j];
       for (int j = 0; j < dim; ++j) Glg[(size_t)i * dim + j] += a * x[j];
     }
@@ -668,9 +703,14 @@ int64_t oracle_pp_step(int64_t n_rows, const int64_t* row_ptr, const int32_t* co
   c.dim = dim;
   c.start = start;
   c.b = b;
-  c.reg = reg;
-  c.reg_exp = reg_exp;
-  c.w = w;
+  c.kind = p->kind;
+  c.reg = p->reg;
+  c.reg_exp = p->reg_exp;
+  c.w = p->w;
+  c.alpha = p->alpha;
+  c.entity_weight = p->entity_weight;
+  c.entity_reg = p->entity_reg;
+  c.other_weight = p->other_weight;
   c.resid = res;
   atomic_init(&c.first_fail, 0);
   run_pool(pp_step_row, &c, n_rows, nthreads, (size_t)2 * b * b + 2 * b);

@@ -108,10 +108,13 @@ int64_t oracle_step(int64_t n_rows, const int64_t* row_ptr,
 void oracle_pp_predict(int64_t n_rows, const int64_t* row_ptr, const int32_t* col,
                        const int32_t* rix, const float* X, int dim, const float* E, float* pred,
                        int nthreads);
+/* p->kind: 0 iALS++ ProjectBlock, 1 SAFER2++ ProjectU (entity_weight),
+ * 2 SAFER2++ ProjectV (entity_reg, other_weight = nu); gram_w weights the
+ * local Gramians (SAFER2++ V step: the dual weights) or NULL. */
 int64_t oracle_pp_step(int64_t n_rows, const int64_t* row_ptr, const int32_t* col,
                        const int32_t* rix, const float* X, int64_t n_other, int dim, float* E,
-                       float* pred, int start, int end, float reg, float reg_exp, float w,
-                       double* residual, int nthreads);
+                       float* pred, int start, int end, const oracle_solve_params* p,
+                       const float* gram_w, double* residual, int nthreads);
 void oracle_user_loss(int64_t n_users, const int64_t* row_ptr,
                       const int32_t* col, const float* U, const float* V,
                       int dim, const float* G, float beta, int half,

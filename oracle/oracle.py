@@ -62,7 +62,7 @@ def lib():
                                        P, P, ctypes.c_int]),
             "oracle_pp_predict": (None, [I64, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int]),
             "oracle_pp_step": (I64, [I64, P, P, P, P, I64, ctypes.c_int, P, P, ctypes.c_int,
-                                     ctypes.c_int, F, F, F, P, ctypes.c_int]),
+                                     ctypes.c_int, P, P, P, ctypes.c_int]),
             "oracle_mt_seed": (None, [P, ctypes.c_uint32]),
             "oracle_mt_next": (ctypes.c_uint32, [P]),
         }
@@ -129,18 +129,25 @@ def pp_predict(row_ptr, col, rix, X, E, pred, nthreads=0):
                             _p(pred), nthreads)
 
 
-def pp_step(row_ptr, col, rix, X, E, pred, start, end, reg, w, reg_exp=1.0, nthreads=0):
-    """iALS++ block Step on columns [start, end): E (float32) and pred updated
-    in place.  Returns (first failing row + 1 or 0, residual)."""
+def pp_step(row_ptr, col, rix, X, E, pred, start, end, reg, w, reg_exp=1.0, kind=0, alpha=0.0,
+            entity_weight=None, entity_reg=None, other_weight=None, gram_w=None, nthreads=0):
+    """iALS++ (kind 0) / SAFER2++ U (1) / V (2) block Step on columns
+    [start, end): E (float32) and pred updated in place.  Returns (first
+    failing row + 1 or 0, residual)."""
     rp = np.ascontiguousarray(row_ptr, np.int64)
     cl = np.ascontiguousarray(col, np.int32)
     rx = np.ascontiguousarray(rix, np.int32)
     X = f32(X)
     assert E.dtype == np.float32 and E.flags.c_contiguous
+    ew = None if entity_weight is None else f32(entity_weight)
+    er = None if entity_reg is None else f32(entity_reg)
+    ow = None if other_weight is None else f32(other_weight)
+    gw = None if gram_w is None else f32(gram_w)
+    sp = SolveParams(kind, reg, reg_exp, w, alpha, 0.0, 0, _p(ew), _p(er), _p(ow))
     res = ctypes.c_double(0.0)
     rc = lib().oracle_pp_step(len(rp) - 1, _p(rp), _p(cl), _p(rx), _p(X), X.shape[0], X.shape[1],
-                              _p(E), _p(pred), start, end, reg, reg_exp, w, ctypes.byref(res),
-                              nthreads)
+                              _p(E), _p(pred), start, end, ctypes.byref(sp), _p(gw),
+                              ctypes.byref(res), nthreads)
     return int(rc), res.value
 
 

@@ -1211,7 +1211,26 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
     return fail(c, FRECSYS_ERR_INVALID, "pp_step: no rating index (pp_set_rating_index)");
   if (!c->d_pred[side == 2 ? 1 : 0])
     return fail(c, FRECSYS_ERR_INVALID, "pp_step: no prediction vector (pp_predict)");
+  const int kind = p->kind;
+  if (kind != FRECSYS_KIND_IALS && kind != FRECSYS_KIND_WEIGHTED_U &&
+      kind != FRECSYS_KIND_WEIGHTED_V)
+    return fail(c, FRECSYS_ERR_INVALID, "pp_step: kind must be IALS, WEIGHTED_U or WEIGHTED_V");
+  if (kind == FRECSYS_KIND_WEIGHTED_V && (!p->entity_reg || !p->other_weight))
+    return fail(c, FRECSYS_ERR_INVALID, "pp_step: WEIGHTED_V needs entity_reg and other_weight");
   HIP_TRY(c, hipSetDevice(c->device));
+  const int other = side == 1 ? 0 : 1;
+  if (kind == FRECSYS_KIND_WEIGHTED_U && p->entity_weight) {
+    int rc = upload(c, &c->d_entity_weight, &c->cap_entity_weight, p->entity_weight,
+                    (size_t)c->n[side]);
+    if (rc) return rc;
+  }
+  if (kind == FRECSYS_KIND_WEIGHTED_V) {
+    int rc = upload(c, &c->d_entity_reg, &c->cap_entity_reg, p->entity_reg, (size_t)c->n[side]);
+    if (rc) return rc;
+    rc = upload(c, &c->d_other_weight, &c->cap_other_weight, p->other_weight,
+                (size_t)c->n[other]);
+    if (rc) return rc;
+  }
   // every rank runs every row: the work queue of the whole side
   const int64_t lo = 0, hi = c->n[side];
   std::vector<QueueRec> recs((size_t)(hi - lo));
@@ -1230,9 +1249,15 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
   a.n_rows = (int64_t)recs.size();
   a.start = start;
   a.bw = end - start;
+  a.kind = kind;
   a.reg = p->reg;
   a.reg_exp = p->reg_exp;
   a.w = p->unobserved_weight;
+  a.alpha = p->alpha;
+  a.entity_weight =
+      (kind == FRECSYS_KIND_WEIGHTED_U && p->entity_weight) ? c->d_entity_weight : nullptr;
+  a.entity_reg = kind == FRECSYS_KIND_WEIGHTED_V ? c->d_entity_reg : nullptr;
+  a.other_weight = kind == FRECSYS_KIND_WEIGHTED_V ? c->d_other_weight : nullptr;
   a.resid = c->d_resid;
   const unsigned long long none = ~0ull;
   HIP_TRY(c, hipMemcpyAsync(c->d_fail, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));

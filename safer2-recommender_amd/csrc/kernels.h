@@ -167,7 +167,11 @@ struct PPArgs {
   const float* G;           // Gramian of the other side, Dp x Dp
   float* E;                 // solved side, ld Dp (block updated in place)
   int Dp, start, bw;        // block columns [start, start + bw), bw <= 128
-  float reg, reg_exp, w;
+  int kind;                 // KIND_IALS (iALS++), KIND_WEIGHTED_U / _V (SAFER2++)
+  float reg, reg_exp, w, alpha;
+  const float* entity_weight;  // U: omega (nullptr -> 1)
+  const float* entity_reg;     // V: item_reg_
+  const float* other_weight;   // V: nu_u = omega_u / |H_u|
   int64_t n_other;
   float* resid;             // [n_rows] squared delta norms, or nullptr
   unsigned long long* fail;

@@ -1,6 +1,7 @@
-// pp.hip -- iALS++ subspace block step on gfx950 (SURVEY 8(f) rank 2;
-// reference ialspp.h: Step :351-424 with ProjectBlock :85-145, and
-// PredictDataset :480-520).
+// pp.hip -- iALS++ / SAFER2++ subspace block step on gfx950 (SURVEY 8(f)
+// rank 2; reference ialspp.h: Step :351-424 with ProjectBlock :85-145, and
+// PredictDataset :480-520; safer2pp.h: StepU / StepV :449-653 with ProjectU
+// :97-160 and ProjectV :162-216).
 //
 // Per block of columns [s, s+bw) (bw = block_size <= 128) and per entity
 // (one workgroup each, LPT queue order):
@@ -8,6 +9,9 @@
 //   r = sum_j x_j,b (pred_j - 1) + w*G[s:e, :] u + lam*u_b
 //   u_b <- u_b - A^-1 r                                 (chol_solve_tiles)
 //   pred_j += (u_b' - u_b) . x_j,b                      (the entity's own ratings)
+// SAFER2++ U: A = (S/h + w*Gl)*omega + lam*I, r = (sum x (pred-1))*omega/h
+// + w*omega*Glg u + lam*u_b; V: rows weighted by nu_u (staged scaled by
+// sqrt(nu)), G = the omega-weighted user Gramian.
 // The block is padded to 32-column tiles (identity on the padded diagonal).
 // pred is the device-resident prediction vector indexed by rating index
 // (position of the tuple in the training file); each rating belongs to one
@@ -39,7 +43,7 @@ __global__ void __launch_bounds__(256) pp_block_kernel(PPArgs a) {
   __shared__ float stage[C::STAGE];
   __shared__ float us[1024];
   __shared__ int ids[32];
-  __shared__ float coef[32];
+  __shared__ float coef[32], ssc[32];
   __shared__ float bvec[BWP], xvec[BWP];
   __shared__ float part[4 * 32];
   __shared__ float red[4];
@@ -49,9 +53,16 @@ __global__ void __launch_bounds__(256) pp_block_kernel(PPArgs a) {
   const QueueRec rec = a.order[blockIdx.x];
   const int64_t e = rec.entity, h = rec.h, p0 = rec.p0;
   if (h == 0) return;
-  const int Dp = a.Dp, s0 = a.start, bw = a.bw;
-  // RegularizationValue(h, num_items) (ialspp.h:377, 313-318)
-  const float lam = a.reg * powf((float)h + a.w * (float)a.n_other, a.reg_exp);
+  const int Dp = a.Dp, s0 = a.start, bw = a.bw, kind = a.kind;
+  const bool uk = kind == KIND_WEIGHTED_U, vk = kind == KIND_WEIGHTED_V;
+  // RegularizationValue (ialspp.h:313-318) / User-, ItemRegularizationValue
+  // (safer2pp.h:425-436)
+  const float lam = entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other,
+                                  a.entity_reg, e);
+  const float omega = (uk && a.entity_weight) ? a.entity_weight[e] : 1.0f;
+  const float hf = (float)h;
+  // U: accumulate S + h*w*Gl, then A = acc * (omega/h) + lam*I
+  const float gsc = uk ? hf * a.w : a.w;
   for (int c = tid; c < Dp; c += 256) us[c] = a.E[e * Dp + c];
   if (tid == 0) flag[0] = 0;
 
@@ -73,7 +84,7 @@ __global__ void __launch_bounds__(256) pp_block_kernel(PPArgs a) {
       float v = 0.0f;
       if (valid[m]) {
         if (gi < bw && gj < bw)
-          v = a.w * a.G[(int64_t)(s0 + gi) * Dp + s0 + gj] + (gi == gj ? lam : 0.0f);
+          v = gsc * a.G[(int64_t)(s0 + gi) * Dp + s0 + gj] + (gi == gj && !uk ? lam : 0.0f);
         else if (gi == gj)
           v = 1.0f;  // padded coordinate: identity
       }
@@ -85,14 +96,26 @@ __global__ void __launch_bounds__(256) pp_block_kernel(PPArgs a) {
     __syncthreads();
     if (tid < 32) {
       const int64_t k = k0 + tid;
-      ids[tid] = k < h ? a.col[p0 + k] : -1;
-      coef[tid] = k < h ? a.pred[a.rix ? a.rix[p0 + k] : p0 + k] - 1.0f : 0.0f;
+      int id = -1;
+      float cf = 0.0f, sa = 0.0f;
+      if (k < h) {
+        id = a.col[p0 + k];
+        cf = a.pred[a.rix ? a.rix[p0 + k] : p0 + k] - 1.0f;
+        sa = 1.0f;
+        if (vk) {  // row staged scaled by sqrt(nu): rhs weight nu / sqrt(nu)
+          sa = sqrtf(a.other_weight[id]);
+          cf *= sa;
+        }
+      }
+      ids[tid] = id;
+      coef[tid] = cf;
+      ssc[tid] = sa;
     }
     __syncthreads();
     for (int i = tid; i < C::STAGE; i += 256) {
       const int r = i / BWP, cc = i % BWP;
       const int id = ids[r];
-      stage[i] = (id >= 0 && cc < bw) ? a.X[(int64_t)id * Dp + s0 + cc] : 0.0f;
+      stage[i] = (id >= 0 && cc < bw) ? a.X[(int64_t)id * Dp + s0 + cc] * ssc[r] : 0.0f;
     }
     __syncthreads();
 #pragma unroll
@@ -117,7 +140,12 @@ __global__ void __launch_bounds__(256) pp_block_kernel(PPArgs a) {
       const int I = (aoff[m] - lo) >> 5, J = (boff[m] - lo) >> 5;
       float* tile = tiles + tidx(I, J) * 1024;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) tile[sw(acc_row(q, hi), lo)] = acc[m][q];
+      for (int q = 0; q < 16; ++q) {
+        const int gi = 32 * I + acc_row(q, hi), gj = 32 * J + lo;
+        float v = acc[m][q];
+        if (uk && gi < bw && gj < bw) v = v * (omega / hf) + (gi == gj ? lam : 0.0f);
+        tile[sw(acc_row(q, hi), lo)] = v;
+      }
     }
   }
   if (tid < BWP) {
@@ -126,7 +154,9 @@ __global__ void __launch_bounds__(256) pp_block_kernel(PPArgs a) {
       const float* g = a.G + (int64_t)(s0 + tid) * Dp;
       float t = 0.0f;
       for (int c = 0; c < Dp; ++c) t += g[c] * us[c];
-      r = bacc + a.w * t + lam * us[s0 + tid];  // ialspp.h:134-137
+      // ialspp.h:134-137; safer2pp.h:143-147, 210-212
+      r = uk ? bacc * (omega / hf) + a.w * t * omega + lam * us[s0 + tid]
+             : bacc + a.w * t + lam * us[s0 + tid];
     }
     bvec[tid] = r;
   }

@@ -273,8 +273,15 @@ class Context:
         self._check(self.lib.frecsys_pp_predict(self.h, side))
 
     def pp_step(self, side: int, start: int, end: int, reg: float, w: float,
-                reg_exp: float = 1.0) -> float:
-        p = _SolveParams(KIND_IALS, reg, reg_exp, w, 0.0, 0.0, 0, 0, None, None, None)
+                reg_exp: float = 1.0, kind: int = 0, alpha: float = 0.0, entity_weight=None,
+                entity_reg=None, other_weight=None) -> float:
+        ew = None if entity_weight is None else np.ascontiguousarray(entity_weight, np.float32)
+        er = None if entity_reg is None else np.ascontiguousarray(entity_reg, np.float32)
+        ow = None if other_weight is None else np.ascontiguousarray(other_weight, np.float32)
+        p = _SolveParams(kind, reg, reg_exp, w, alpha, 0.0, 0, 0,
+                         None if ew is None else ew.ctypes.data,
+                         None if er is None else er.ctypes.data,
+                         None if ow is None else ow.ctypes.data)
         res = ctypes.c_double(0.0)
         self._check(self.lib.frecsys_pp_step(self.h, side, start, end, ctypes.byref(p),
                                              ctypes.byref(res)))

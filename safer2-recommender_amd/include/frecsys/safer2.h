@@ -231,7 +231,7 @@ class SAFER2Recommender : public detail::DeviceModel {
  protected:
   void OnEmbeddingsSet() override { dev_->Gramian(DeviceContext::ITEM); }
 
- private:
+ protected:
   // ComputeUserWeights (safer2.h:745-794): only users with a history.
   void ComputeUserWeights(const Dataset& data) {
     const Csr& uc = data.user_csr();

@@ -9,8 +9,8 @@
 // std::random_device), --device (HIP ordinal), --parity_quirks (0/1,
 // SURVEY App. A.1).  One process per GPU for multi-GPU runs: WORLD_SIZE /
 // RANK / LOCAL_RANK from the environment (torchrun-style), RCCL id through
-// FRECSYS_COMM_FILE.  iALS++ (ialspp.h) runs on the GPU block-step kernels;
-// SAFER2++ (safer2pp.h) is not part of this build.
+// FRECSYS_COMM_FILE.  iALS++ / SAFER2++ (ialspp.h, safer2pp.h) run on the
+// GPU block-step kernels.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -24,6 +24,7 @@
 #include "frecsys/ials.h"
 #include "frecsys/ialspp.h"
 #include "frecsys/safer2.h"
+#include "frecsys/safer2pp.h"
 
 namespace {
 
@@ -127,6 +128,12 @@ frecsys::Recommender* get_model(const std::string& name, int num_users, int num_
         a.i("--pd_iterations"), a.b("--use_epanechnikov"), a.b("--use_snr"),
         a.f("--sampling_ratio"), a.b("--use_cg"), a.f("--cg_error_tolerance"),
         a.i("--cg_max_iterations"), o);
+  } else if (name == "safer2pp") {
+    r = new frecsys::SAFER2ppRecommender(
+        a.i("--dim"), num_users, num_items, a.f("--l2_reg"), a.f("--uobs_weight"),
+        a.f("--bandwidth"), a.f("--alpha"), a.f("--stdev"), a.i("--xi_iterations"),
+        a.i("--pd_iterations"), a.b("--use_epanechnikov"), a.b("--use_snr"),
+        a.f("--sampling_ratio"), a.i("--block_size"), o);
   } else if (name == "erm_mf") {
     r = new frecsys::ERMMFRecommender(a.i("--dim"), num_users, num_items, a.f("--l2_reg"),
                                       a.f("--uobs_weight"), a.f("--stdev"), a.f("--alpha"),
@@ -137,7 +144,7 @@ frecsys::Recommender* get_model(const std::string& name, int num_users, int num_
                                        a.f("--uobs_weight"), a.f("--alpha"), a.f("--stepsize"),
                                        a.f("--stdev"), o);
   } else {
-    LOG(FATAL) << "model " << name << " (SAFER2++) is not part of this build";
+    LOG(FATAL) << "model " << name << " is not part of this build";
   }
   r->SetPrintResidualStats(a.b("--print_residual_stats"));
   r->SetPrintVarStats(a.b("--print_var_stats"));
@@ -211,6 +218,8 @@ int main(int argc, char* argv[]) {
 
   if (model_name == "cvar_mf") ((frecsys::CVaRMFRecommender*)recommender)->Initialize(train);
   if (model_name == "safer2") ((frecsys::SAFER2Recommender*)recommender)->Initialize(train);
+  if (model_name == "safer2pp")
+    ((frecsys::SAFER2ppRecommender*)recommender)->Initialize(train);
   if (model_name == "erm_mf") ((frecsys::ERMMFRecommender*)recommender)->Initialize(train);
   const int epochs = app.i("--epoch");
   const bool print_eval = app.b("--print_evaluation_stats");

@@ -108,3 +108,53 @@ def test_gate_ialspp_run_model():  # ialspp_test.cc:14-80
     m = re.search(r"Mean NDCG@20=([0-9.]+)", tail)
     assert m and float(m.group(1)) >= 0.2, tail[-2000:]
     assert len(re.findall(r"U residual: [0-9.e+-]+, V residual", r.stderr)) == 10
+
+
+@pytest.mark.parametrize("dim,bs", [(8, 4), (64, 32), (128, 128)])
+def test_safer2pp_blocks_match_oracle(quirk_data, dim, bs):
+    """SAFER2++ StepU / StepV (safer2pp.h:449-653): weighted block steps."""
+    from test_parity_gpu import _v_inputs, _weights
+    nu, ni, up, uc, ip, ic = quirk_data
+    reg, w, alpha = 0.004, 0.004, 0.3
+    ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+    om = _weights(nu)
+    nu_w, item_reg = _v_inputs(nu, ni, up, ip, ic, om)
+    urix, irix = _rix(uc)
+    ctx.pp_set_rating_index(fh.SIDE_USER, urix)
+    ctx.pp_set_rating_index(fh.SIDE_ITEM, irix)
+    ctx.pp_predict(fh.SIDE_USER)
+    pred = np.zeros(len(uc), np.float32)
+    O.pp_predict(up, uc, urix, V, U, pred)
+    Uo, Vo = U.copy(), V.copy()
+    for start in range(0, dim, bs):
+        end = min(start + bs, dim)
+        ctx.gramian(fh.SIDE_ITEM)
+        ctx.pp_step(fh.SIDE_USER, start, end, reg, w, kind=fh.KIND_WEIGHTED_U, entity_weight=om)
+        rc, _ = O.pp_step(up, uc, urix, Vo, Uo, pred, start, end, reg, w, kind=1,
+                          entity_weight=om)
+        assert rc == 0
+        ctx.gramian(fh.SIDE_USER, weights=om)
+        ctx.pp_step(fh.SIDE_ITEM, start, end, reg, w, kind=fh.KIND_WEIGHTED_V, alpha=alpha,
+                    entity_reg=item_reg, other_weight=nu_w)
+        rc, _ = O.pp_step(ip, ic, irix, Uo, Vo, pred, start, end, reg, w, kind=2, alpha=alpha,
+                          entity_reg=item_reg, other_weight=nu_w, gram_w=om)
+        assert rc == 0
+    assert rel_rows(ctx.get_embeddings(fh.SIDE_USER), Uo).max() < TOL_ROW
+    assert rel_rows(ctx.get_embeddings(fh.SIDE_ITEM), Vo).max() < TOL_ROW
+
+
+def test_gate_safer2pp_run_model():  # safer2pp_test.cc:100-145
+    cmd = [os.path.join(PKG, "bin", "run_model"), "--train_data", os.path.join(ML1M, "train.csv"),
+           "--test_train_data", os.path.join(ML1M, "validation_tr.csv"),
+           "--test_test_data", os.path.join(ML1M, "validation_te.csv"), "--seed", "1",
+           "--model_name", "safer2pp", "--dim", "8", "--block_size", "4", "--uobs_weight",
+           "0.004", "--l2_reg", "0.004", "--bandwidth", "0.15", "--alpha", "0.3",
+           "--xi_iterations", "5", "--pd_iterations", "1", "--epoch", "10",
+           "--print_var_stats", "1", "--print_train_stats", "1", "--print_residual_stats", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    tail = r.stderr[r.stderr.rindex("Validation Results"):]
+    m = re.search(r"Mean NDCG@20=([0-9.]+)", tail)
+    assert m and float(m.group(1)) >= 0.2, tail[-2000:]
+    means = [float(x) for x in re.findall(r"Min: [0-9.]+, Mean: ([0-9.]+), Max", r.stderr)]
+    assert len(means) == 10 and all(abs(x - 0.3) <= 0.02 for x in means), means
