@@ -67,6 +67,9 @@ struct DualCfg {
   static constexpr int OFF_FLAG = OFF_PART + PART;
   static constexpr int OFF_L = OFF_FLAG + 4;        // l_k [Dp], then D^-1/2 [Dp]
   static constexpr int NQ = (HP * 8 + NTHR - 1) / NTHR;  // float4 per thread per slab
+  // waves per SIMD the register allocation must allow (TH = 3: 4 workgroups
+  // per CU, TH = 4: 3 -- their LDS allows it; the bigger buckets are LDS-bound)
+  static constexpr int WPE = (TH == 3) ? 4 : (TH == 4 ? 3 : 1);
   static constexpr size_t bytes(int Dp) { return (size_t)(OFF_L + 2 * Dp) * 4; }
   static_assert(bytes(kMaxDp) <= 163840, "LDS budget");
 };
@@ -143,7 +146,8 @@ __global__ void __launch_bounds__(256) dual_sweep_kernel(DualArgs a) {
 }
 
 template <int TH>
-__global__ void __launch_bounds__(DualCfg<TH>::NTHR) dual_solve_kernel(DualArgs a) {
+__global__ void __launch_bounds__(DualCfg<TH>::NTHR)
+    __attribute__((amdgpu_waves_per_eu(DualCfg<TH>::WPE, 8))) dual_solve_kernel(DualArgs a) {
   using C = DualCfg<TH>;
   constexpr int HP = C::HP, NT = C::NT, NW = C::NW, NTHR = C::NTHR, MT = C::MT;
   constexpr int SROW = C::SROW, NQ = C::NQ;
