@@ -119,6 +119,14 @@ int frecsys_partition(int64_t n_rows, const int64_t* row_ptr, int32_t nparts,
                       int64_t* bounds);
 /* RCCL unique id (128 bytes) -- call on rank 0, broadcast to the others. */
 int frecsys_comm_unique_id(uint8_t id[128]);
+/* Join rank `rank` of `world`.  id != NULL: RCCL communicator; the library
+ * all-reduces the Gramians and all-gathers factor rows / losses itself.
+ * id == NULL (world > 1): external exchange -- no communicator; every call
+ * works on this rank's shard only (frecsys_gramian returns the partial Gramian
+ * over the rank's rows, solve_side / user_loss write only its rows) and the
+ * caller performs the exchange (frecsys_set_gramian, set_embeddings), e.g.
+ * over its own MPI / gloo transport or, in tests, several contexts of one
+ * process sharing a device. */
 int frecsys_comm_init(frecsys_ctx* ctx, int32_t world, int32_t rank,
                       const uint8_t id[128]);
 /* Row range [lo, hi) of `side` owned by this rank (after load_csr). */

@@ -326,7 +326,7 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
 // Row-range all-gather of a [rows x ld] float matrix (uneven per-rank
 // counts): every rank broadcasts its own range in place.
 int allgather_rows(frecsys_ctx* c, float* base, int side, int64_t ld) {
-  if (c->world == 1) return FRECSYS_OK;
+  if (c->world == 1 || !c->comm) return FRECSYS_OK;  // external exchange: the caller's
   NCCL_TRY(c, ncclGroupStart());
   for (int r = 0; r < c->world; ++r) {
     const int64_t lo = c->bounds[side][r], hi = c->bounds[side][r + 1];
@@ -619,7 +619,7 @@ int frecsys_comm_init(frecsys_ctx* c, int32_t world, int32_t rank, const uint8_t
   }
   c->world = world;
   c->rank = rank;
-  if (world > 1) {
+  if (world > 1 && id) {
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
     NCCL_TRY(c, ncclCommInitRank(&c->comm, world, uid, rank));
@@ -774,7 +774,7 @@ int frecsys_gramian(frecsys_ctx* c, int32_t side, const float* weights, int32_t 
     HIP_TRY(c, launch_gramian(c->Dp, g, c->stream));
     t.stop();
   }
-  if (c->world > 1) {
+  if (c->world > 1 && c->comm) {
     ScopedTimer t(c, "allreduce");
     NCCL_TRY(c, ncclAllReduce(c->gram[side], c->gram[side], (size_t)c->Dp * c->Dp, ncclFloat,
                               ncclSum, c->comm, c->stream));
@@ -1033,6 +1033,13 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
     }
     t.stop();
   }
+  const bool collective = side < 2 && c->world > 1 && c->comm;
+  if (collective) {
+    // every rank takes the same retry / NOT_SPD decision below (the
+    // smallest failing entity over all ranks), so the collectives of a
+    // rerun stay matched
+    NCCL_TRY(c, ncclAllReduce(c->d_fail, c->d_fail, 1, ncclUint64, ncclMin, c->comm, c->stream));
+  }
   unsigned long long f = none;
   HIP_TRY(c, hipMemcpyAsync(&f, c->d_fail, sizeof(f), hipMemcpyDeviceToHost, c->stream));
   if (side < 2 && c->world > 1) {
@@ -1056,7 +1063,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
               (double)hp[16 * t + 2] / n, (double)hp[16 * t + 3] / n);
     }
   }
-  if (f != none && dual && n_dspace < n_nonempty) {
+  if (f != none && dual && (collective || n_dspace < n_nonempty)) {
     // a history-space pivot failed: the verdict is the d-space solve's
     return solve_side_impl(c, side, p, true);
   }

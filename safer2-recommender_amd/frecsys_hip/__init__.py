@@ -185,8 +185,10 @@ class Context:
         self.close()
 
     # -- comm --
-    def comm_init(self, world: int, rank: int, uid: bytes):
-        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+    def comm_init(self, world: int, rank: int, uid: Optional[bytes]):
+        """uid None: external exchange (no RCCL; the caller moves partial
+        Gramians and shard rows between ranks)."""
+        buf = None if uid is None else (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         self._check(self.lib.frecsys_comm_init(self.h, world, rank, buf))
 
     def shard_range(self, side: int) -> Tuple[int, int]:
@@ -226,6 +228,11 @@ class Context:
         self._check(self.lib.frecsys_gramian(self.h, side, _ptr(w), 1 if from_snapshot else 0,
                                              _ptr(out)))
         return out
+
+    def set_gramian(self, side: int, G: np.ndarray):
+        g = np.ascontiguousarray(G, dtype=np.float32)
+        assert g.shape == (self.dim, self.dim), g.shape
+        self._check(self.lib.frecsys_set_gramian(self.h, side, _ptr(g), self.dim))
 
     def solve_side(self, side: int, kind: int, reg: float, unobserved_weight: float,
                    reg_exp: float = 1.0, alpha: float = 0.0, stepsize: float = 0.0,
