@@ -216,5 +216,8 @@ hipError_t launch_gram_dot(const float* A, const float* B, int Dp, double* dot, 
 // Padded leading dimension for a logical dimension (8, 16, multiples of 32
 // up to 256, then 512 and 1024).  Returns 0 when unsupported.
 int padded_dim(int dim);
+// true (default): the SYRK kernels run fp32-accurate split-bf16 MFMA
+// (common.h mfma_x6); FRECSYS_SYRK_F32=1 selects v_mfma_f32_32x32x2_f32.
+bool syrk_split_bf16();
 
 }  // namespace frecsys_hip

@@ -40,19 +40,27 @@ namespace {
 
 constexpr int kRing = 4;
 
-template <int T>
+// BF = true: the SYRK runs on the bf16 matrix cores with 3-piece split
+// operands (common.h mfma_x6, fp32-accurate).  Chunks of R = 32 rows, staged
+// as pieces in a k-major image: 16-B granule (piece p, row group g of 16,
+// k-half hh, column c) holds rows 16g + 8hh .. +7 of column c -- exactly the
+// bf16x8 fragment lane (c & 31, hh) of v_mfma_f32_32x32x16_bf16 reads; lanes
+// read consecutive granules (no bank conflicts).  One thread per (column,
+// row group) gathers its 16 values, splits them and writes 6 granules.
+template <int T, bool BF>
 struct TiledCfg {
   static constexpr int Dp = 32 * T;
   static constexpr int NT = T * (T + 1) / 2;
   static constexpr int NW = (T <= 2) ? 4 : 8;       // waves per workgroup
   static constexpr int NTHR = NW * 64;
   static constexpr int MT = (NT + NW - 1) / NW;     // tiles per wave (max)
-  static constexpr int R = (T <= 2) ? 16 : (T >= 8 ? 64 : 32);  // rows per staged chunk
+  static constexpr int R = BF ? 32 : ((T <= 2) ? 16 : (T >= 8 ? 64 : 32));  // rows per chunk
   static constexpr int NSLOT = R * Dp / 4;          // float4 per chunk
   static constexpr int NQ = (NSLOT + NTHR - 1) / NTHR;
+  static constexpr int GRAN = 12 * Dp;              // BF: 16-B granules per stage buffer
   // LDS carve (floats); every offset a multiple of 4 floats (16 B).
   static constexpr int TILES = NT * 1024;
-  static constexpr int STAGE = 2 * R * Dp;          // aliases TILES
+  static constexpr int STAGE = BF ? 2 * 4 * GRAN : 2 * R * Dp;  // aliases TILES
   static constexpr int REGION0 = TILES > STAGE ? TILES : STAGE;
   static constexpr int OFF_B = REGION0;             // rhs, then y
   static constexpr int OFF_X = OFF_B + Dp;          // e (CVaR), then x
@@ -65,7 +73,15 @@ struct TiledCfg {
   static constexpr size_t BYTES = (size_t)TOTAL * 4;
   static_assert(BYTES <= 163840, "LDS budget");
   static_assert(R % 2 == 0, "row pairs");
+  static_assert(!BF || 2 * Dp <= NTHR, "BF: one thread per (column, row group)");
 };
+
+// Granule index (16 B) of piece p, row group g, k-half hh, column c in one
+// BF stage buffer.
+template <int Dp>
+__device__ __forceinline__ int bf_gran(int p, int g, int hh, int c) {
+  return ((p * 2 + g) * 2 + hh) * Dp + c;
+}
 
 // Virtual history position k -> offset within the entity's CSR row: k < h
 // are the real rows; with the tail quirk rows h .. h+extra-1 re-read the
@@ -81,10 +97,10 @@ __device__ __forceinline__ int64_t virt_pos(int64_t k, int64_t h) {
 // own workgroup (PARTIAL = false, a.split[pos].y > 0) then starts from the
 // sum of its slabs instead of gathering -- the longest histories (55K rows
 // on the ML-20M item side) no longer serialise on one CU.
-template <int T, bool PARTIAL>
-__global__ void __launch_bounds__(TiledCfg<T>::NTHR)
+template <int T, bool PARTIAL, bool BF>
+__global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     solve_tiled_kernel(SolveArgs a) {
-  using C = TiledCfg<T>;
+  using C = TiledCfg<T, BF>;
   constexpr int Dp = C::Dp, NT = C::NT, NW = C::NW, NTHR = C::NTHR, MT = C::MT;
   constexpr int R = C::R, NQ = C::NQ, NSLOT = C::NSLOT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -156,36 +172,99 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     ring_sa[s] = sa;
     ring_bw[s] = bw;
   };
-  float4 regs[NQ];
-  auto load_data = [&](int c) {
-    const int slot = c % kRing;
+  // BF gather: thread (column bc, row group bg) of the chunk
+  // (row group wave-uniform when Dp is a multiple of 64; threads past 2*Dp
+  // gather row group 0 again and never store -- branch-free loads)
+  const int bc = tid % Dp;
+  const bool bown = BF && tid < 2 * Dp;
+  const int bg = bown ? tid / Dp : 0;
+  float xr[BF ? 16 : 1];
+  float bpart = 0.0f;  // BF: this thread's rhs part for column bc
+  auto load_bf = [&](int c) {
+    if constexpr (BF) {
+      const int4* ids = reinterpret_cast<const int4*>(ring_id + (c % kRing) * R + 16 * bg);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int sidx = tid + q * NTHR;
-      regs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (NSLOT % NTHR == 0 || sidx < NSLOT) {
-        const int r = sidx / (Dp / 4), c4 = sidx % (Dp / 4);
-        const int id = ring_id[slot * R + r];
-        if (id >= 0) regs[q] = *reinterpret_cast<const float4*>(a.X + (int64_t)id * Dp + 4 * c4);
+      for (int q = 0; q < 4; ++q) {
+        const int4 id4 = ids[q];
+        const int id[4] = {id4.x, id4.y, id4.z, id4.w};
+        // no select on the loaded value: rows past the history have sa = 0
+        // (store_bf), so the loads stay in flight through the MFMA phase
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xr[4 * q + j] = a.X[(int64_t)max(id[j], 0) * Dp + bc];
+      }
+    }
+  };
+  auto store_bf = [&](int buf, int c) {
+    if constexpr (BF) {
+      // rows pre-scaled by sa (1 for non-V kinds, 0 past the history), rhs
+      // weight bw per scaled row -- as the fp32 staging below
+      const int base = (c % kRing) * R + 16 * bg;
+      float sa[16], bw[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 s4 = reinterpret_cast<const float4*>(ring_sa + base)[q];
+        const float4 w4 = reinterpret_cast<const float4*>(ring_bw + base)[q];
+        sa[4 * q] = s4.x, sa[4 * q + 1] = s4.y, sa[4 * q + 2] = s4.z, sa[4 * q + 3] = s4.w;
+        bw[4 * q] = w4.x, bw[4 * q + 1] = w4.y, bw[4 * q + 2] = w4.z, bw[4 * q + 3] = w4.w;
+      }
+      bf16x8* st = reinterpret_cast<bf16x8*>(stage) + buf * C::GRAN;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = xr[8 * hh + j] * sa[8 * hh + j];
+          bpart += bw[8 * hh + j] * x;
+          v[j] = x;
+        }
+        bf16x8 f[3];
+        split3x8(v, f);
+        if (bown) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) st[bf_gran<Dp>(p, bg, hh, bc)] = f[p];
+        }
+      }
+    }
+  };
+  constexpr int NQR = BF ? 1 : NQ;
+  float4 regs[NQR];
+  auto load_data = [&](int c) {
+    if constexpr (BF) {
+      load_bf(c);
+    } else {
+      const int slot = c % kRing;
+#pragma unroll
+      for (int q = 0; q < NQR; ++q) {
+        const int sidx = tid + q * NTHR;
+        regs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (NSLOT % NTHR == 0 || sidx < NSLOT) {
+          const int r = sidx / (Dp / 4), c4 = sidx % (Dp / 4);
+          const int id = ring_id[slot * R + r];
+          if (id >= 0) regs[q] = *reinterpret_cast<const float4*>(a.X + (int64_t)id * Dp + 4 * c4);
+        }
       }
     }
   };
   auto store_stage = [&](int buf, int c) {
-    float* st = stage + buf * R * Dp;
-    const int slot = c % kRing;
+    if constexpr (BF) {
+      store_bf(buf, c);
+    } else {
+      float* st = stage + buf * R * Dp;
+      const int slot = c % kRing;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int sidx = tid + q * NTHR;
-      if (NSLOT % NTHR == 0 || sidx < NSLOT) {
-        float4 v = regs[q];
-        if (vk) {
-          const float sc = ring_sa[slot * R + sidx / (Dp / 4)];
-          v.x *= sc;
-          v.y *= sc;
-          v.z *= sc;
-          v.w *= sc;
+      for (int q = 0; q < NQR; ++q) {
+        const int sidx = tid + q * NTHR;
+        if (NSLOT % NTHR == 0 || sidx < NSLOT) {
+          float4 v = regs[q];
+          if (vk) {
+            const float sc = ring_sa[slot * R + sidx / (Dp / 4)];
+            v.x *= sc;
+            v.y *= sc;
+            v.z *= sc;
+            v.w *= sc;
+          }
+          *reinterpret_cast<float4*>(st + 4 * sidx) = v;
         }
-        *reinterpret_cast<float4*>(st + 4 * sidx) = v;
       }
     }
   };
@@ -269,28 +348,56 @@ __global__ void __launch_bounds__(TiledCfg<T>::NTHR)
     int nid = -1;
     float nsa = 0.f, nbw = 0.f;
     if (ring_more) ring_load(c + 2, nid, nsa, nbw);
-    const float* st = stage + buf * R * Dp;
-    const int slot = c % kRing;
-    // tile-outer, row-pair-inner: one wave-uniform branch per tile and the
-    // operand reads free to run ahead of the MFMAs
-    if (!(a.debug_skip & 1)) {
+    if constexpr (BF) {
+      const bf16x8* st = reinterpret_cast<const bf16x8*>(stage) + buf * C::GRAN;
+      if (!(a.debug_skip & 1)) {
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        if (valid[m]) {
+        for (int m = 0; m < MT; ++m) {
+          if (valid[m]) {
 #pragma unroll
-          for (int s = 0; s < R / 2; ++s) {
-            const float* rowp = st + (2 * s + hi) * Dp;
-            acc[m] = mfma32(rowp[aoff[m]], rowp[boff[m]], acc[m]);
+            for (int g = 0; g < 2; ++g) {
+              bf16x8 av[3], bv[3];
+#pragma unroll
+              for (int p = 0; p < 3; ++p) {
+                av[p] = st[bf_gran<Dp>(p, g, hi, aoff[m])];
+                bv[p] = st[bf_gran<Dp>(p, g, hi, boff[m])];
+              }
+              acc[m] = mfma_x6(av, bv, acc[m]);
+            }
           }
         }
       }
-    }
-    if (tid < Dp) {
+    } else {
+      const float* st = stage + buf * R * Dp;
+      const int slot = c % kRing;
+      // tile-outer, row-pair-inner: one wave-uniform branch per tile and the
+      // operand reads free to run ahead of the MFMAs
+      if (!(a.debug_skip & 1)) {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          if (valid[m]) {
+#pragma unroll
+            for (int s = 0; s < R / 2; ++s) {
+              const float* rowp = st + (2 * s + hi) * Dp;
+              acc[m] = mfma32(rowp[aoff[m]], rowp[boff[m]], acc[m]);
+            }
+          }
+        }
+      }
+      if (tid < Dp) {
 #pragma unroll 4
-      for (int r = 0; r < R; ++r) bacc += ring_bw[slot * R + r] * st[r * Dp + tid];
+        for (int r = 0; r < R; ++r) bacc += ring_bw[slot * R + r] * st[r * Dp + tid];
+      }
     }
     if (more) store_stage(buf ^ 1, c + 1);
     if (ring_more) ring_store(c + 2, nid, nsa, nbw);
+    lds_barrier();
+  }
+  if constexpr (BF) {
+    // rhs: the two row groups' parts of each column (the stage is dead)
+    if (bown && bg == 1) part[bc] = bpart;
+    lds_barrier();
+    if (tid < Dp) bacc += bpart + part[tid];
     lds_barrier();
   }
 
@@ -490,21 +597,27 @@ __global__ void __launch_bounds__(256) solve_small_kernel(SolveArgs a) {
   if (!ok) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
-template <int T, bool PARTIAL>
-hipError_t launch_tiled(const SolveArgs& a, hipStream_t s) {
-  using C = TiledCfg<T>;
+template <int T, bool PARTIAL, bool BF>
+hipError_t launch_tiled_v(const SolveArgs& a, hipStream_t s) {
+  using C = TiledCfg<T, BF>;
   static bool attr = false;
   if (!attr) {
-    hipError_t err = hipFuncSetAttribute((const void*)solve_tiled_kernel<T, PARTIAL>,
+    hipError_t err = hipFuncSetAttribute((const void*)solve_tiled_kernel<T, PARTIAL, BF>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)C::BYTES);
     if (err != hipSuccess) return err;
     attr = true;
   }
   const int64_t n = PARTIAL ? a.n_work : a.n_rows;
-  hipLaunchKernelGGL((solve_tiled_kernel<T, PARTIAL>), dim3((unsigned)n), dim3(C::NTHR), C::BYTES,
-                     s, a);
+  hipLaunchKernelGGL((solve_tiled_kernel<T, PARTIAL, BF>), dim3((unsigned)n), dim3(C::NTHR),
+                     C::BYTES, s, a);
   return hipGetLastError();
+}
+
+template <int T, bool PARTIAL>
+hipError_t launch_tiled(const SolveArgs& a, hipStream_t s) {
+  return syrk_split_bf16() ? launch_tiled_v<T, PARTIAL, true>(a, s)
+                           : launch_tiled_v<T, PARTIAL, false>(a, s);
 }
 
 template <int Dp>
@@ -515,6 +628,14 @@ hipError_t launch_small(const SolveArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+bool syrk_split_bf16() {
+  static const bool on = [] {
+    const char* v = getenv("FRECSYS_SYRK_F32");
+    return !(v && atoi(v) != 0);
+  }();
+  return on;
+}
 
 int padded_dim(int dim) {
   if (dim <= 0) return 0;
