@@ -28,8 +28,9 @@
 //     row stride): each row's lane runs the bidiagonal recurrence
 //     z_j[k] = y_j[k] - l_k z_j[k-1] across the slab (carry in a register)
 //     and writes D^-1/2-scaled values k-major; the waves then accumulate
-//     their S tiles with v_mfma_f32_32x32x2_f32 while the next slab's loads
-//     are in flight;
+//     their S tiles while the next slab's loads are in flight -- by default
+//     on the bf16 matrix cores with fp32-accurate 3-piece split operands
+//     (common.h mfma_x6), FRECSYS_SYRK_F32=1: v_mfma_f32_32x32x2_f32;
 //   * S tiles go to LDS (aliasing the slab buffers), chol_solve_tiles, then
 //     Y^T (c.*z) re-reads the (cache-resident) rows with float4 loads.
 #include <hip/hip_runtime.h>
@@ -44,7 +45,17 @@ namespace {
 
 constexpr int kMaxDp = 1024;
 
-template <int TH>
+// BF = true: S accumulates on the bf16 matrix cores with 3-piece split
+// operands (common.h mfma_x6, fp32-accurate): the recurrence lane of row j
+// writes its 32 scaled slab values as pieces, 16-B granule (piece p, k group
+// g of 16, k-half hh, row j) = the bf16x8 fragment lane (j & 31, hh) of
+// v_mfma_f32_32x32x16_bf16 reads (dgran below).
+template <int HP>
+__device__ __forceinline__ int dgran(int p, int g, int hh, int j) {
+  return ((p * 2 + g) * 2 + hh) * HP + j;
+}
+
+template <int TH, bool BF>
 struct DualCfg {
   static constexpr int HP = 32 * TH;                // padded history rows
   static constexpr int NT = TH * (TH + 1) / 2;      // lower tiles of S
@@ -53,7 +64,7 @@ struct DualCfg {
   static constexpr int MT = (NT + NW - 1) / NW;
   static constexpr int SROW = 33;                   // slab row stride
   static constexpr int STG = HP * SROW;
-  static constexpr int ZS = 32 * HP;                // k-major scaled Z slab
+  static constexpr int ZS = (BF ? 48 : 32) * HP;   // k-major scaled Z slab (BF: pieces)
   static constexpr int TILES = NT * 1024;
   static constexpr int NSTAGE = (TH <= 4) ? 1 : 2;  // LDS stages for the slab prefetch
   static constexpr int LOOP = ((NSTAGE * STG + ZS + 3) / 4) * 4;
@@ -68,8 +79,9 @@ struct DualCfg {
   static constexpr int OFF_L = OFF_FLAG + 4;        // l_k [Dp], then D^-1/2 [Dp]
   static constexpr int NQ = (HP * 8 + NTHR - 1) / NTHR;  // float4 per thread per slab
   // waves per SIMD the register allocation must allow (TH = 3: 4 workgroups
-  // per CU, TH = 4: 3 -- their LDS allows it; the bigger buckets are LDS-bound)
-  static constexpr int WPE = (TH == 3) ? 4 : (TH == 4 ? 3 : 1);
+  // of 4 waves per CU, TH = 4: 3 of 4, TH = 5: 2 of 8 -- their LDS allows
+  // it; the bigger buckets are LDS-bound)
+  static constexpr int WPE = (TH == 3 || TH == 5) ? 4 : (TH == 4 ? 3 : 1);
   static constexpr size_t bytes(int Dp) { return (size_t)(OFF_L + 2 * Dp) * 4; }
   static_assert(bytes(kMaxDp) <= 163840, "LDS budget");
 };
@@ -145,10 +157,10 @@ __global__ void __launch_bounds__(256) dual_sweep_kernel(DualArgs a) {
   }
 }
 
-template <int TH>
-__global__ void __launch_bounds__(DualCfg<TH>::NTHR)
-    __attribute__((amdgpu_waves_per_eu(DualCfg<TH>::WPE, 8))) dual_solve_kernel(DualArgs a) {
-  using C = DualCfg<TH>;
+template <int TH, bool BF>
+__global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
+    __attribute__((amdgpu_waves_per_eu(DualCfg<TH, BF>::WPE, 8))) dual_solve_kernel(DualArgs a) {
+  using C = DualCfg<TH, BF>;
   constexpr int HP = C::HP, NT = C::NT, NW = C::NW, NTHR = C::NTHR, MT = C::MT;
   constexpr int SROW = C::SROW, NQ = C::NQ;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -275,27 +287,66 @@ __global__ void __launch_bounds__(DualCfg<TH>::NTHR)
     if (c + 2 < NC) load_slab(c + 2, mine);
     if (tid < HP && !(a.debug_skip & 128)) {
       const float* yrow = stage + ((c & 1) % C::NSTAGE) * C::STG + tid * SROW;
-      float y[32];
+      float y[BF ? 1 : 32];
+      if constexpr (!BF) {
 #pragma unroll
-      for (int kk = 0; kk < 32; ++kk) y[kk] = yrow[kk];
+        for (int kk = 0; kk < 32; ++kk) y[kk] = yrow[kk];
+      }
       float z = carry;
+      if constexpr (BF) {
+        bf16x8* zb = reinterpret_cast<bf16x8*>(zs);
 #pragma unroll
-      for (int kk = 0; kk < 32; ++kk) {
-        const int k = 32 * c + kk;
-        z = y[kk] - lsub[k] * z;
-        zs[kk * HP + tid] = (cj * z) * dsq[k];
+        for (int gh = 0; gh < 4; ++gh) {  // (k group, k-half) = 8 consecutive k
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int kk = 8 * gh + u, k = 32 * c + kk;
+            z = yrow[kk] - lsub[k] * z;
+            v[u] = (cj * z) * dsq[k];
+          }
+          bf16x8 f[3];
+          split3x8(v, f);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) zb[dgran<HP>(p, gh >> 1, gh & 1, tid)] = f[p];
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 32; ++kk) {
+          const int k = 32 * c + kk;
+          z = y[kk] - lsub[k] * z;
+          zs[kk * HP + tid] = (cj * z) * dsq[k];
+        }
       }
       carry = z;
     }
     lds_barrier();
     if (!(a.debug_skip & 1)) {
+      if constexpr (BF) {
+        const bf16x8* zb = reinterpret_cast<const bf16x8*>(zs);
 #pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        if (valid[m]) {  // wave-uniform
+        for (int m = 0; m < MT; ++m) {
+          if (valid[m]) {  // wave-uniform
 #pragma unroll
-          for (int s = 0; s < 16; ++s) {
-            const float* zr = zs + (2 * s + hi) * HP;
-            acc[m] = mfma32(zr[aoff[m]], zr[boff[m]], acc[m]);
+            for (int g = 0; g < 2; ++g) {
+              bf16x8 av[3], bv[3];
+#pragma unroll
+              for (int p = 0; p < 3; ++p) {
+                av[p] = zb[dgran<HP>(p, g, hi, aoff[m])];
+                bv[p] = zb[dgran<HP>(p, g, hi, boff[m])];
+              }
+              acc[m] = mfma_x6(av, bv, acc[m]);
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          if (valid[m]) {  // wave-uniform
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+              const float* zr = zs + (2 * s + hi) * HP;
+              acc[m] = mfma32(zr[aoff[m]], zr[boff[m]], acc[m]);
+            }
           }
         }
       }
@@ -449,11 +500,11 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
   wave_sync();
 }
 
-template <int TH>
+template <int TH, bool BF>
 struct WaveCfg {
   static constexpr int HP = 32 * TH;
   static constexpr int NT = TH * (TH + 1) / 2;
-  static constexpr int ZS = 32 * HP;
+  static constexpr int ZS = (BF ? 48 : 32) * HP;
   static constexpr int REG = NT * 1024 > ZS ? NT * 1024 : ZS;
   static constexpr int OFF_ID = REG, OFF_C = OFF_ID + HP, OFF_B = OFF_C + HP, OFF_X = OFF_B + HP;
   static constexpr int OFF_FLAG = OFF_X + HP;
@@ -463,9 +514,9 @@ struct WaveCfg {
   static_assert(TH <= 2, "one history row per lane");
 };
 
-template <int TH>
+template <int TH, bool BF>
 __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
-  using C = WaveCfg<TH>;
+  using C = WaveCfg<TH, BF>;
   constexpr int HP = C::HP, NT = C::NT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63;
@@ -542,28 +593,68 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
     if (c + 1 < NC) load(c + 1, yn);
     if (j < HP) {
       float z = carry;
+      if constexpr (BF) {
+        bf16x8* zb = reinterpret_cast<bf16x8*>(zs);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float yv[4] = {yr[q].x, yr[q].y, yr[q].z, yr[q].w};
+        for (int gh = 0; gh < 4; ++gh) {  // 8 consecutive k: float4 pairs 2gh, 2gh+1
+          float v[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int kk = 4 * q + u, k = 32 * c + kk;
-          z = yv[u] - trow[k] * z;
-          zs[kk * HP + j] = (cj * z) * trow[Dp + k];
+          for (int u = 0; u < 8; ++u) {
+            const float4 y4 = yr[2 * gh + (u >> 2)];
+            const float yv = (u & 3) == 0 ? y4.x : (u & 3) == 1 ? y4.y : (u & 3) == 2 ? y4.z : y4.w;
+            const int k = 32 * c + 8 * gh + u;
+            z = yv - trow[k] * z;
+            v[u] = (cj * z) * trow[Dp + k];
+          }
+          bf16x8 f[3];
+          split3x8(v, f);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) zb[dgran<HP>(p, gh >> 1, gh & 1, j)] = f[p];
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float yv[4] = {yr[q].x, yr[q].y, yr[q].z, yr[q].w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int kk = 4 * q + u, k = 32 * c + kk;
+            z = yv[u] - trow[k] * z;
+            zs[kk * HP + j] = (cj * z) * trow[Dp + k];
+          }
         }
       }
       carry = z;
     }
     wave_sync();
+    if constexpr (BF) {
+      // each row block's pieces once, reused by every tile it takes part in
+      const bf16x8* zb = reinterpret_cast<const bf16x8*>(zs);
 #pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2) {
-      const float* zr = zs + (2 * s2 + hi) * HP;
+      for (int g = 0; g < 2; ++g) {
+        bf16x8 fr[TH][3];
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        int I = 0;
-        while ((I + 1) * (I + 2) / 2 <= t) ++I;
-        const int J = t - I * (I + 1) / 2;
-        acc[t] = mfma32(zr[32 * I + lo], zr[32 * J + lo], acc[t]);
+        for (int b = 0; b < TH; ++b)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) fr[b][p] = zb[dgran<HP>(p, g, hi, 32 * b + lo)];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          int I = 0;
+          while ((I + 1) * (I + 2) / 2 <= t) ++I;
+          const int J = t - I * (I + 1) / 2;
+          acc[t] = mfma_x6(fr[I], fr[J], acc[t]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) {
+        const float* zr = zs + (2 * s2 + hi) * HP;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          int I = 0;
+          while ((I + 1) * (I + 2) / 2 <= t) ++I;
+          const int J = t - I * (I + 1) / 2;
+          acc[t] = mfma32(zr[32 * I + lo], zr[32 * J + lo], acc[t]);
+        }
       }
     }
     wave_sync();
@@ -622,28 +713,38 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   if (lane == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
-template <int TH>
-hipError_t launch_wave_t(const DualArgs& a, hipStream_t s) {
-  using C = WaveCfg<TH>;
+template <int TH, bool BF>
+hipError_t launch_wave_v(const DualArgs& a, hipStream_t s) {
+  using C = WaveCfg<TH, BF>;
   const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
-  hipLaunchKernelGGL(dual_wave_kernel<TH>, dim3(nb), dim3(256), C::bytes(a.Dp), s, a);
+  hipLaunchKernelGGL((dual_wave_kernel<TH, BF>), dim3(nb), dim3(256), C::bytes(a.Dp), s, a);
   return hipGetLastError();
 }
 
 template <int TH>
-hipError_t launch_dual_t(const DualArgs& a, hipStream_t s) {
-  using C = DualCfg<TH>;
+hipError_t launch_wave_t(const DualArgs& a, hipStream_t s) {
+  return syrk_split_bf16() ? launch_wave_v<TH, true>(a, s) : launch_wave_v<TH, false>(a, s);
+}
+
+template <int TH, bool BF>
+hipError_t launch_dual_v(const DualArgs& a, hipStream_t s) {
+  using C = DualCfg<TH, BF>;
   static bool attr = false;
   if (!attr) {
-    hipError_t err = hipFuncSetAttribute((const void*)dual_solve_kernel<TH>,
+    hipError_t err = hipFuncSetAttribute((const void*)dual_solve_kernel<TH, BF>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)C::bytes(kMaxDp));
     if (err != hipSuccess) return err;
     attr = true;
   }
-  hipLaunchKernelGGL(dual_solve_kernel<TH>, dim3((unsigned)a.n_rows), dim3(C::NTHR),
+  hipLaunchKernelGGL((dual_solve_kernel<TH, BF>), dim3((unsigned)a.n_rows), dim3(C::NTHR),
                      C::bytes(a.Dp), s, a);
   return hipGetLastError();
+}
+
+template <int TH>
+hipError_t launch_dual_t(const DualArgs& a, hipStream_t s) {
+  return syrk_split_bf16() ? launch_dual_v<TH, true>(a, s) : launch_dual_v<TH, false>(a, s);
 }
 
 }  // namespace
