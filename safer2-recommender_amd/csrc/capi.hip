@@ -1059,8 +1059,10 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       const unsigned long long n = hp[16 * t + 4];
       if (!n) continue;
       fprintf(stderr, "[dual-prof] side %d tiles %d n %llu cycles/entity: setup %.0f slabs %.0f chol %.0f "
-              "yz %.0f\n", side, t, n, (double)hp[16 * t] / n, (double)hp[16 * t + 1] / n,
-              (double)hp[16 * t + 2] / n, (double)hp[16 * t + 3] / n);
+              "yz %.0f | chain %.0f workers %.0f factored %.0f\n", side, t, n,
+              (double)hp[16 * t] / n, (double)hp[16 * t + 1] / n, (double)hp[16 * t + 2] / n,
+              (double)hp[16 * t + 3] / n, (double)hp[16 * t + 5] / n, (double)hp[16 * t + 6] / n,
+              (double)hp[16 * t + 7] / n);
     }
   }
   if (f != none && dual && (collective || n_dspace < n_nonempty)) {

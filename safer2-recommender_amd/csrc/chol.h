@@ -5,6 +5,12 @@
 
 #include "common.h"
 
+// 1 (default): the d-space and history-space kernels factor with the
+// dataflow chol_solve_df; 0: the barrier-phased chol_solve_tiles.
+#ifndef FRECSYS_CHOL_DF
+#define FRECSYS_CHOL_DF 1
+#endif
+
 namespace frecsys_hip {
 
 __device__ __forceinline__ float rdlane(float v, int l) {
@@ -35,7 +41,8 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
   float a[32];
 #pragma unroll
   for (int c = 0; c < 32; ++c) {
-    const float t = tile[sw(r, c)];  // both halves read (no divergent loads)
+    float t = tile[sw(r, c)];  // both halves read (no divergent loads)
+    asm volatile("" : "+v"(t));  // keeps the load out of a per-element branch
     a[c] = fl ? t : (c == r ? 1.0f : 0.0f);
   }
   bool ok = true;
@@ -197,6 +204,200 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
     }
     lds_barrier();
   }
+}
+
+// ---------------------------------------------------------------------
+// Dataflow variant of chol_solve_tiles (same inputs, outputs and scratch
+// contract; part[] must hold 2T + T(T+1)/2 + 2 ints and 32 floats).  The
+// blocked factorisation and both substitutions are tile tasks
+//   F(p)      factor + invert diagonal tile (p, p)
+//   Y(p)      y_p = L_pp^-1 b_p                       (b_p fully updated)
+//   S(I, p)   TRSM  L_Ip = A_Ip (L_pp^-1)^T                       (I > p)
+//   B(I, p)   b_I -= L_Ip y_p                                     (I > p)
+//   U(I,J,p)  A_IJ -= L_Ip L_Jp^T                         (p < J <= I)
+// ordered by LDS version counters instead of workgroup barriers: ver(I,J)
+// = updates applied to tile (I, J), +1 once final (TRSM'd / factored);
+// bver(I) = updates applied to b_I; yver = y blocks published.  Wave 0
+// runs only the critical chain
+//   F(p), Y(p) -> S(p+1, p), B(p+1, p) -> U(p+1, p+1, p) -> F(p+1), ...
+// (at raised issue priority); the other waves take the remaining S+B and
+// U tasks of each panel round-robin, next-column tiles first.  Every wave
+// walks its tasks in one global order (panel by panel: chain, S+B, U by
+// column) in which each task's dependencies come earlier, so the waits
+// cannot deadlock.  The backward sweep x = L^-T y runs the same way after
+// one barrier: wave 0 publishes x_q = L_qq^-T (r_q - L_{q+1,q}^T x_{q+1}),
+// the workers fold x_q into r_p (p <= q - 2, each r_p owned by one worker,
+// rcnt(p) = x blocks folded in).
+// debug_skip masks (ablation only): 2 diag, 4 TRSM, 8 trailing.
+// ---------------------------------------------------------------------
+typedef __attribute__((address_space(3))) int lds_int;
+
+__device__ __forceinline__ int ld_ver(const int* f) {
+  return __builtin_amdgcn_readfirstlane(*(volatile lds_int*)(f));
+}
+__device__ __forceinline__ void wait_ver(const int* f, int v) {
+  if (ld_ver(f) < v) {
+    do {
+      __builtin_amdgcn_s_sleep(1);
+    } while (ld_ver(f) < v);
+  }
+  asm volatile("" ::: "memory");
+}
+// publish: all of this wave's LDS writes land before the counter
+__device__ __forceinline__ void set_ver(int* f, int v, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lane == 0) *(volatile lds_int*)(f) = v;
+  asm volatile("" ::: "memory");
+}
+
+// One wave: sum_m M(lo, m) v[m] (TR: M(m, lo)) of a swizzled tile and a
+// 32-vector in LDS; lane (lo, hi) takes half hi of m, both halves get the
+// total.
+template <bool TR>
+__device__ __forceinline__ float tile_gemv(const float* M, const float* v, int lo, int hi) {
+  float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+  for (int m = 0; m < 16; m += 2) {
+    const int m0 = 16 * hi + m;
+    s0 += M[TR ? sw(m0, lo) : sw(lo, m0)] * v[m0];
+    s1 += M[TR ? sw(m0 + 1, lo) : sw(lo, m0 + 1)] * v[m0 + 1];
+  }
+  const float s = s0 + s1;
+  return s + __shfl_xor(s, 32);
+}
+
+template <int T, int NW>
+__device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* xvec,
+                                              float* part, int* flag, int tid, int debug_skip,
+                                              unsigned long long* prof = nullptr) {
+  static_assert(NW >= 2, "one chain wave and at least one worker");
+  constexpr int NT = T * (T + 1) / 2;
+  const unsigned long long t0 = prof ? clock64() : 0;
+  const int lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int* ver = reinterpret_cast<int*>(part);
+  int* bver = ver + NT;
+  int* rcnt = bver + T;
+  int* yver = rcnt + T;
+  int* xver = yver + 1;
+  float* rbuf = part + ((NT + 2 * T + 2 + 3) & ~3);  // 32 floats: wave 0's r_p
+  if (tid < NT + 2 * T + 2) ver[tid] = 0;
+  lds_barrier();
+
+  auto trsm = [&](int I, int p) {  // S(I, p)
+    float* Aip = tiles + tidx(I, p) * 1024;
+    if (!(debug_skip & 4)) {
+      const f32x16 u = tile_pqT(Aip, tiles + tidx(p, p) * 1024, lo, hi);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) Aip[sw(acc_row(q, hi), lo)] = u[q];
+    }
+    set_ver(ver + tidx(I, p), p + 1, lane);
+  };
+  auto bupd = [&](int I, int p) {  // B(I, p): L_Ip final, y_p published
+    wait_ver(bver + I, p);
+    const float t = tile_gemv<false>(tiles + tidx(I, p) * 1024, bvec + 32 * p, lo, hi);
+    if (hi == 0) bvec[32 * I + lo] -= t;
+    set_ver(bver + I, p + 1, lane);
+  };
+  auto update = [&](int I, int J, int p) {  // U(I, J, p)
+    float* Aij = tiles + tidx(I, J) * 1024;
+    if (!(debug_skip & 8)) {
+      const f32x16 u = tile_pqT(tiles + tidx(I, p) * 1024, tiles + tidx(J, p) * 1024, lo, hi);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) Aij[sw(acc_row(q, hi), lo)] -= u[q];
+    }
+    set_ver(ver + tidx(I, J), p + 1, lane);
+  };
+  auto factor_y = [&](int p) {  // F(p), then Y(p) (b_p final: bver(p) = p)
+    float* Tpp = tiles + tidx(p, p) * 1024;
+    if (!(debug_skip & 2)) {
+      if (!diag_factor_inv(Tpp, lane) && lane == 0) flag[0] = 1;
+    }
+    set_ver(ver + tidx(p, p), p + 1, lane);
+    const float y = tile_gemv<false>(Tpp, bvec + 32 * p, lo, hi);
+    wave_lds_sync();
+    if (hi == 0) bvec[32 * p + lo] = y;
+    set_ver(yver, p + 1, lane);
+  };
+
+  if (wave == 0) {
+    // ---- the critical chain (issue priority over the worker on its SIMD) ----
+    __builtin_amdgcn_s_setprio(2);
+    factor_y(0);
+#pragma unroll 1
+    for (int p = 0; p + 1 < T; ++p) {
+      wait_ver(ver + tidx(p + 1, p), p);  // all of panel < p's updates
+      trsm(p + 1, p);
+      bupd(p + 1, p);
+      wait_ver(ver + tidx(p + 1, p + 1), p);
+      update(p + 1, p + 1, p);
+      factor_y(p + 1);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (prof && lane == 0) atomicAdd(prof + 5, clock64() - t0);
+  } else {
+    // ---- workers: the rest of each panel, round-robin ----
+    int k = 0;
+#pragma unroll 1
+    for (int p = 0; p + 1 < T; ++p) {
+#pragma unroll 1
+      for (int I = p + 2; I < T; ++I, ++k) {  // S(I, p), B(I, p)
+        if (1 + k % (NW - 1) != wave) continue;
+        wait_ver(ver + tidx(p, p), p + 1);
+        wait_ver(ver + tidx(I, p), p);
+        trsm(I, p);
+        wait_ver(yver, p + 1);
+        bupd(I, p);
+      }
+#pragma unroll 1
+      for (int J = p + 1; J < T; ++J) {  // U(I, J, p), column by column
+#pragma unroll 1
+        for (int I = (J == p + 1 ? p + 2 : J); I < T; ++I, ++k) {
+          if (1 + k % (NW - 1) != wave) continue;
+          wait_ver(ver + tidx(I, p), p + 1);
+          wait_ver(ver + tidx(J, p), p + 1);
+          wait_ver(ver + tidx(I, J), p);
+          update(I, J, p);
+        }
+      }
+    }
+    if (prof && lane == 0) atomicAdd(prof + 6, (clock64() - t0) / (NW - 1));
+  }
+  lds_barrier();
+  if (prof && tid == 0) atomicAdd(prof + 7, clock64() - t0);
+
+  // ---- backward: x = L^-T y; bvec holds y and, per block, r_p ----
+  if (wave == 0) {
+    __builtin_amdgcn_s_setprio(2);
+#pragma unroll 1
+    for (int p = T - 1; p >= 0; --p) {
+      float r = bvec[32 * p + lo];
+      if (p + 1 < T) {
+        wait_ver(rcnt + p, T - 2 - p);  // x_q, q >= p + 2, folded in by a worker
+        r = bvec[32 * p + lo] -
+            tile_gemv<true>(tiles + tidx(p + 1, p) * 1024, xvec + 32 * (p + 1), lo, hi);
+      }
+      if (hi == 0) rbuf[lo] = r;
+      wave_lds_sync();
+      const float x = tile_gemv<true>(tiles + tidx(p, p) * 1024, rbuf, lo, hi);
+      if (hi == 0) xvec[32 * p + lo] = x;
+      set_ver(xver, T - p, lane);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  } else {
+#pragma unroll 1
+    for (int q = T - 1; q >= 2; --q) {
+#pragma unroll 1
+      for (int p = 0; p + 2 <= q; ++p) {
+        if (1 + p % (NW - 1) != wave) continue;
+        wait_ver(xver, T - q);
+        const float t = tile_gemv<true>(tiles + tidx(q, p) * 1024, xvec + 32 * q, lo, hi);
+        if (hi == 0) bvec[32 * p + lo] -= t;
+        set_ver(rcnt + p, T - q, lane);
+      }
+    }
+  }
+  lds_barrier();
 }
 
 }  // namespace frecsys_hip

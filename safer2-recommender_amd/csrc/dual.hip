@@ -375,7 +375,11 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   }
   lds_barrier();
   mark(1);
+#if FRECSYS_CHOL_DF
+  chol_solve_df<TH, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip, a.prof);
+#else
   chol_solve_tiles<TH, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
+#endif
   mark(2);
 
   // ---- v = Y^T (c.*z): the rows again, float4 per lane, 8 rows in flight ----

@@ -461,7 +461,11 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
   }
 
   // ---- blocked right-looking Cholesky with lookahead + back-solve ----
+#if FRECSYS_CHOL_DF
+  chol_solve_df<T, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
+#else
   chol_solve_tiles<T, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
+#endif
   if (tid < Dp) a.out[e * Dp + tid] = xvec[tid];
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }

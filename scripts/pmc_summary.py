@@ -34,7 +34,7 @@ for name in sorted(set(fetch) | set(write)):
 # the d-space solve (roofline kernel): launches alternate user, item in
 # every bench epoch (warmup included); averaged over all launches
 for name, v in summary["kernels"].items():
-    if "solve_tiled_kernel<8, false>" in name:
+    if "solve_tiled_kernel<8, false" in name:  # <8, false> / <8, false, BF>
         tot = [a + b for a, b in zip(v["fetch_bytes_per_launch"], v["write_bytes_per_launch"])]
         summary["dspace_traffic_bytes"] = sum(tot) / max(1, len(tot))
         summary["dspace_user_traffic_bytes"] = sum(tot[0::2]) / max(1, len(tot[0::2]))
