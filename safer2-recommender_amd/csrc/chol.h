@@ -323,14 +323,15 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   if (wave == 0) {
     // ---- the critical chain (issue priority over the worker on its SIMD) ----
     __builtin_amdgcn_s_setprio(2);
-    factor_y(0);
 #pragma unroll 1
-    for (int p = 0; p + 1 < T; ++p) {
-      wait_ver(ver + tidx(p + 1, p), p);  // all of panel < p's updates
-      trsm(p + 1, p);
-      bupd(p + 1, p);
-      wait_ver(ver + tidx(p + 1, p + 1), p);
-      update(p + 1, p + 1, p);
+    for (int p = -1; p + 1 < T; ++p) {  // one factor_y call site
+      if (p >= 0) {
+        wait_ver(ver + tidx(p + 1, p), p);  // all of panel < p's updates
+        trsm(p + 1, p);
+        bupd(p + 1, p);
+        wait_ver(ver + tidx(p + 1, p + 1), p);
+        update(p + 1, p + 1, p);
+      }
       factor_y(p + 1);
     }
     __builtin_amdgcn_s_setprio(0);
