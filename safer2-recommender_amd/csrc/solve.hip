@@ -178,9 +178,8 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
   const int bc = tid % Dp;
   const bool bown = BF && tid < 2 * Dp;
   const int bg = bown ? tid / Dp : 0;
-  float xr[BF ? 16 : 1];
   float bpart = 0.0f;  // BF: this thread's rhs part for column bc
-  auto load_bf = [&](int c) {
+  auto load_bf = [&](int c, float (&xr)[16]) {
     if constexpr (BF) {
       const int4* ids = reinterpret_cast<const int4*>(ring_id + (c % kRing) * R + 16 * bg);
 #pragma unroll
@@ -188,13 +187,17 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
         const int4 id4 = ids[q];
         const int id[4] = {id4.x, id4.y, id4.z, id4.w};
         // no select on the loaded value: rows past the history have sa = 0
-        // (store_bf), so the loads stay in flight through the MFMA phase
+        // (split_bf), so the loads stay in flight through the MFMA phase
 #pragma unroll
         for (int j = 0; j < 4; ++j) xr[4 * q + j] = a.X[(int64_t)max(id[j], 0) * Dp + bc];
       }
     }
   };
-  auto store_bf = [&](int buf, int c) {
+  // split_bf: the pieces of chunk c in registers (the math only, so it can
+  // share a basic block with -- and be scheduled between -- the MFMAs of
+  // the previous chunk); write_bf: the granule stores.  `live` = false
+  // (past the last chunk) leaves the rhs part untouched.
+  auto split_bf = [&](int c, const float (&xr)[16], bf16x8 (&f)[2][3], bool live) {
     if constexpr (BF) {
       // rows pre-scaled by sa (1 for non-V kinds, 0 past the history), rhs
       // weight bw per scaled row -- as the fp32 staging below
@@ -207,31 +210,54 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
         sa[4 * q] = s4.x, sa[4 * q + 1] = s4.y, sa[4 * q + 2] = s4.z, sa[4 * q + 3] = s4.w;
         bw[4 * q] = w4.x, bw[4 * q + 1] = w4.y, bw[4 * q + 2] = w4.z, bw[4 * q + 3] = w4.w;
       }
-      bf16x8* st = reinterpret_cast<bf16x8*>(stage) + buf * C::GRAN;
+      float bsum = 0.0f;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         float v[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float x = xr[8 * hh + j] * sa[8 * hh + j];
-          bpart += bw[8 * hh + j] * x;
+          bsum += bw[8 * hh + j] * x;
           v[j] = x;
         }
-        bf16x8 f[3];
-        split3x8(v, f);
-        if (bown) {
+        split3x8(v, f[hh]);
+      }
+      bpart = live ? bpart + bsum : bpart;
+    }
+  };
+  auto scale_bf = [&](int c, const float (&xr)[16], float (&xs)[16], bool live) {
+    if constexpr (BF) {
+      const int base = (c % kRing) * R + 16 * bg;
+      float bsum = 0.0f;
 #pragma unroll
-          for (int p = 0; p < 3; ++p) st[bf_gran<Dp>(p, bg, hh, bc)] = f[p];
+      for (int q = 0; q < 4; ++q) {
+        const float4 s4 = reinterpret_cast<const float4*>(ring_sa + base)[q];
+        const float4 w4 = reinterpret_cast<const float4*>(ring_bw + base)[q];
+        const float sa[4] = {s4.x, s4.y, s4.z, s4.w}, bw[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xs[4 * q + j] = xr[4 * q + j] * sa[j];
+          bsum += bw[j] * xs[4 * q + j];
         }
+      }
+      bpart = live ? bpart + bsum : bpart;
+    }
+  };
+  auto write_bf = [&](int buf, const bf16x8 (&f)[2][3]) {
+    if constexpr (BF) {
+      bf16x8* st = reinterpret_cast<bf16x8*>(stage) + buf * C::GRAN;
+      if (bown) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) st[bf_gran<Dp>(p, bg, hh, bc)] = f[hh][p];
       }
     }
   };
   constexpr int NQR = BF ? 1 : NQ;
   float4 regs[NQR];
-  auto load_data = [&](int c) {
-    if constexpr (BF) {
-      load_bf(c);
-    } else {
+  auto load_data = [&](int c) {  // fp32 path
+    {
       const int slot = c % kRing;
 #pragma unroll
       for (int q = 0; q < NQR; ++q) {
@@ -245,10 +271,8 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
       }
     }
   };
-  auto store_stage = [&](int buf, int c) {
-    if constexpr (BF) {
-      store_bf(buf, c);
-    } else {
+  auto store_stage = [&](int buf, int c) {  // fp32 path
+    {
       float* st = stage + buf * R * Dp;
       const int slot = c % kRing;
 #pragma unroll
@@ -270,14 +294,15 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
   };
 
   if (tid == 0) flag[0] = 0;
-  if (tid < R && nchunks > 0) {
-    int id;
-    float sa, bw;
-    ring_load(0, id, sa, bw);
-    ring_store(0, id, sa, bw);
-    if (nchunks > 1) {
-      ring_load(1, id, sa, bw);
-      ring_store(1, id, sa, bw);
+  if (tid < R) {  // ring prologue: the chunks the first iteration reads
+#pragma unroll
+    for (int c = 0; c < (BF ? 3 : 2); ++c) {
+      if (c < nchunks) {
+        int id;
+        float sa, bw;
+        ring_load(c, id, sa, bw);
+        ring_store(c, id, sa, bw);
+      }
     }
   }
   if (!PARTIAL && is_grad_kind(kind) && tid < Dp) xvec[tid] = a.E[e * Dp + tid];
@@ -334,26 +359,62 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     if (tid < Dp) bacc += sl[NT * 1024 + tid];
   }
   lds_barrier();
-  if (nchunks > 0) {
-    load_data(0);
-    store_stage(0, 0);
-  }
-  lds_barrier();
-
-  for (int c = 0; c < nchunks; ++c) {
-    const int buf = c & 1;
-    const bool more = c + 1 < nchunks;
-    const bool ring_more = (tid < R) && (c + 2 < nchunks);
-    if (more) load_data(c + 1);
-    int nid = -1;
-    float nsa = 0.f, nbw = 0.f;
-    if (ring_more) ring_load(c + 2, nid, nsa, nbw);
-    if constexpr (BF) {
+  if constexpr (BF) {
+    // two chunks of row loads in flight: iteration c runs the MFMAs of
+    // chunk c, stages chunk c+1 (registers xcur, loaded one iteration ago)
+    // and issues chunk c+2's loads into xnxt -- a full iteration of cover
+    // for the gather latency; the ring is filled three chunks ahead
+    float xa[16], xb[16];
+    if (nchunks > 0) {
+      load_bf(0, xa);
+      bf16x8 f[2][3];
+      split_bf(0, xa, f, true);
+      write_bf(0, f);
+    }
+    if (nchunks > 1) load_bf(1, xa);
+    lds_barrier();
+    auto step = [&](int c, float (&xcur)[16], float (&xnxt)[16]) {
+      const int buf = c & 1;
+      if (c + 2 < nchunks) load_bf(c + 2, xnxt);
+      const bool ring_more = (tid < R) && (c + 3 < nchunks);
+      int nid = -1;
+      float nsa = 0.f, nbw = 0.f;
+      if (ring_more) ring_load(c + 3, nid, nsa, nbw);
+      const bool live = c + 1 < nchunks;
+      // chunk c+1's staging math is spread over the issue gaps of this
+      // chunk's MFMAs: scaled values (and the rhs part) first, then two
+      // 3-piece splits after each mfma_x6 of the tiles every wave has
+      float xs[16];
+      scale_bf(c + 1, xcur, xs, live);
+      bf16x8 f[2][3];
+      constexpr int SLOTS = (NT / NW) * 2 > 0 ? (NT / NW) * 2 : 1;
+      constexpr int PER = (16 + SLOTS - 1) / SLOTS;
+      auto split_slot = [&](int slot) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int j = slot * PER + u;
+          if (j < 16) {
+            __bf16 h, m, l;
+            split3(xs[j], h, m, l);
+            f[j >> 3][0][j & 7] = h;
+            f[j >> 3][1][j & 7] = m;
+            f[j >> 3][2][j & 7] = l;
+          }
+        }
+        // keep this slot's pieces here (between the MFMAs), not sunk to
+        // their stores after the loop
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+          if ((slot * PER) >> 3 == hh || (slot * PER + PER - 1) >> 3 == hh)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(f[hh][p]));
+      };
       const bf16x8* st = reinterpret_cast<const bf16x8*>(stage) + buf * C::GRAN;
       if (!(a.debug_skip & 1)) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          if (valid[m]) {
+          // tiles every wave has: no branch, one basic block with the splits
+          if (m < NT / NW || valid[m]) {
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
               bf16x8 av[3], bv[3];
@@ -363,11 +424,37 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
                 bv[p] = st[bf_gran<Dp>(p, g, hi, boff[m])];
               }
               acc[m] = mfma_x6(av, bv, acc[m]);
+              if (m < NT / NW) split_slot(2 * m + g);
             }
           }
         }
+        if constexpr (NT / NW == 0) split_slot(0);
+      } else {
+#pragma unroll
+        for (int k = 0; k < SLOTS; ++k) split_slot(k);
       }
-    } else {
+      if (live) write_bf(buf ^ 1, f);
+      if (ring_more) ring_store(c + 3, nid, nsa, nbw);
+      lds_barrier();
+    };
+    for (int c = 0; c < nchunks; c += 2) {
+      step(c, xa, xb);
+      if (c + 1 < nchunks) step(c + 1, xb, xa);
+    }
+  } else {
+    if (nchunks > 0) {
+      load_data(0);
+      store_stage(0, 0);
+    }
+    lds_barrier();
+    for (int c = 0; c < nchunks; ++c) {
+      const int buf = c & 1;
+      const bool more = c + 1 < nchunks;
+      const bool ring_more = (tid < R) && (c + 2 < nchunks);
+      if (more) load_data(c + 1);
+      int nid = -1;
+      float nsa = 0.f, nbw = 0.f;
+      if (ring_more) ring_load(c + 2, nid, nsa, nbw);
       const float* st = stage + buf * R * Dp;
       const int slot = c % kRing;
       // tile-outer, row-pair-inner: one wave-uniform branch per tile and the
@@ -388,10 +475,10 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
 #pragma unroll 4
         for (int r = 0; r < R; ++r) bacc += ring_bw[slot * R + r] * st[r * Dp + tid];
       }
+      if (more) store_stage(buf ^ 1, c + 1);
+      if (ring_more) ring_store(c + 2, nid, nsa, nbw);
+      lds_barrier();
     }
-    if (more) store_stage(buf ^ 1, c + 1);
-    if (ring_more) ring_store(c + 2, nid, nsa, nbw);
-    lds_barrier();
   }
   if constexpr (BF) {
     // rhs: the two row groups' parts of each column (the stage is dead)
