@@ -15,10 +15,12 @@ fixed, so scaling is "strong".
 value = users updated per second of training wall time = N_users * K / T,
 T = max over ranks of the K-epoch wall time.  sec_per_epoch = T / K.
 
-roofline: the dominant kernel is solve_tiled_kernel<8, false>, the d x d
-solve of the long histories (h > 256; the shorter ones take the
-history-space path): gather + MFMA assembly + blocked
-Cholesky, compute-bound, priced against the fp32 MFMA peak (157.3 TFLOP/s).
+roofline: the dominant kernel is solve_tiled_kernel<8, false, true>, the
+d x d solve of the long histories (h > 256; the shorter ones take the
+history-space path): gather + MFMA assembly (its fp32
+products on the bf16 matrix cores as 3-piece splits, fp32-accurate) +
+dataflow blocked Cholesky, compute-bound, priced against the fp32 MFMA
+peak (157.3 TFLOP/s) since the algorithm is fp32.
 Algorithmic flops per launch = sum over its entities of h*d*(d+1) (0 for
 the histories > 2048 rows whose SYRK the split kernel did) + d^3/3 + 2*d^2
 (SURVEY 8(d)); duration = its HIP-event time (both half-steps averaged).
@@ -247,7 +249,9 @@ def main():
                        "parallelism": f"entity-sharded x{world}"},
             "u_halfstep_solve_updates_per_s": (n_own / (su_ms * 1e-3)) * world if su_ms else None,
             "kernel_ms_per_epoch": {k: v[0] / max(K, 1) for k, v in timers.items()},
-            "roofline": {"bound": "mfma", "kernel": "solve_tiled_kernel<8, false> (d-space solve)",
+            "roofline": {"bound": "mfma",
+                         "kernel": "solve_tiled_kernel<8, false, true> (d-space solve: split-bf16 "
+                                   "MFMA SYRK + fp32 dataflow Cholesky)",
                          "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
                          "traffic_source": traffic_src,
