@@ -10,6 +10,10 @@
 #ifndef FRECSYS_CHOL_DF
 #define FRECSYS_CHOL_DF 1
 #endif
+// 1 (default): diagonal blocks by diag_factor_inv_blk (MFMA cross terms).
+#ifndef FRECSYS_DIAG_BLK
+#define FRECSYS_DIAG_BLK 1
+#endif
 
 namespace frecsys_hip {
 
@@ -77,7 +81,98 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
   return ok;
 }
 
+// Blocked form of the same factor + inverse: columns 0..15 by the
+// recurrence above (rows 16..31 come out as L21), then the cross terms of
+// every lane's columns 16..31 -- sum_{m<16} L[16+c][m] v[m], the Schur
+// update A22 -= L21 L21^T for the rows and the L21 X1 coupling for the
+// inverse columns alike -- as one 64 x 16 x 16 product on the matrix cores
+// (16 v_mfma_f32_16x16x4_f32, operands through the tile, whose values are
+// in registers by then), and columns 16..31 by the recurrence over
+// m in [16, k) only.  256 v_readlane + 256 FMAs of the serial chain become
+// MFMAs.
+__device__ __noinline__ bool diag_factor_inv_blk(lds_float* tile, int lane) {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const int r = lane & 31;
+  const bool fl = lane < 32;
+  float a[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) {
+    float t = tile[sw(r, c)];
+    asm volatile("" : "+v"(t));
+    a[c] = fl ? t : (c == r ? 1.0f : 0.0f);
+  }
+  bool ok = true;
+  auto column = [&](int k, int m0) {  // column k from the terms m in [m0, k)
+    float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+#pragma unroll
+    for (int m = m0; m < k; m += 4) {
+      const float b0 = rdlane(a[m], k);
+      const float b1 = m + 1 < k ? rdlane(a[m + 1], k) : 0.0f;
+      const float b2 = m + 2 < k ? rdlane(a[m + 2], k) : 0.0f;
+      const float b3 = m + 3 < k ? rdlane(a[m + 3], k) : 0.0f;
+      p0 += a[m] * b0;
+      if (m + 1 < k) p1 += a[m + 1] * b1;
+      if (m + 2 < k) p2 += a[m + 2] * b2;
+      if (m + 3 < k) p3 += a[m + 3] * b3;
+    }
+    const float t = a[k] - ((p0 + p1) + (p2 + p3));
+    const float piv = rdlane(t, k);
+    ok = ok && (piv > 0.0f);
+    a[k] = t * __builtin_amdgcn_rsqf(piv);  // lane k: t = piv -> sqrt(piv)
+  };
+#pragma unroll
+  for (int k = 0; k < 16; ++k) column(k, 0);
+  // ---- cross terms on the matrix cores ----
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  lds_float* U = tile;  // [64][16]: lane l's a[0..15]; rows 16..31 = L21
+#pragma unroll
+  for (int m = 0; m < 16; m += 4)
+    *reinterpret_cast<__attribute__((address_space(3))) f32x4*>(U + lane * 16 + m) =
+        f32x4{a[m], a[m + 1], a[m + 2], a[m + 3]};
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int li = lane & 15, lk = lane >> 4;
+  f32x4 w[4] = {f32x4{0.f}, f32x4{0.f}, f32x4{0.f}, f32x4{0.f}};
+#pragma unroll
+  for (int k0 = 0; k0 < 4; ++k0) {
+    // A[i][k] = L21[i][4k0+k], B[k][n] = U[16nb+n][4k0+k]; D[c'][n] -> W[16nb+n][c']
+    const float av = U[(16 + li) * 16 + 4 * k0 + lk];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      const float bv = U[(16 * nb + li) * 16 + 4 * k0 + lk];
+      w[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, w[nb], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // U's reads done before W overwrites it
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+    *reinterpret_cast<__attribute__((address_space(3))) f32x4*>(U + (16 * nb + li) * 16 + 4 * lk) =
+        w[nb];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int c = 0; c < 16; c += 4) {
+    const f32x4 x = *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(
+        U + lane * 16 + c);
+    a[16 + c] -= x[0];
+    a[17 + c] -= x[1];
+    a[18 + c] -= x[2];
+    a[19 + c] -= x[3];
+  }
+#pragma unroll
+  for (int k = 16; k < 32; ++k) column(k, 16);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int j = r;
+#pragma unroll
+  for (int k = 0; k < 32; ++k)
+    if (!fl) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
+  return ok;
+}
+
+// BLK = true for kernels with a register budget above ~150 VGPRs (the
+// blocked form needs more registers than the plain one; a call counts
+// toward the caller's allocation, so a capped kernel would lose occupancy).
+template <bool BLK = false>
 __device__ __forceinline__ bool diag_factor_inv(float* tile, int lane) {
+  if constexpr (BLK && FRECSYS_DIAG_BLK) return diag_factor_inv_blk((lds_float*)tile, lane);
   return diag_factor_inv_lds((lds_float*)tile, lane);
 }
 
@@ -266,7 +361,7 @@ __device__ __forceinline__ float tile_gemv(const float* M, const float* v, int l
   return s + __shfl_xor(s, 32);
 }
 
-template <int T, int NW>
+template <int T, int NW, bool BLK = true>
 __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* xvec,
                                               float* part, int* flag, int tid, int debug_skip,
                                               unsigned long long* prof = nullptr) {
@@ -311,7 +406,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   auto factor_y = [&](int p) {  // F(p), then Y(p) (b_p final: bver(p) = p)
     float* Tpp = tiles + tidx(p, p) * 1024;
     if (!(debug_skip & 2)) {
-      if (!diag_factor_inv(Tpp, lane) && lane == 0) flag[0] = 1;
+      if (!diag_factor_inv<BLK>(Tpp, lane) && lane == 0) flag[0] = 1;
     }
     set_ver(ver + tidx(p, p), p + 1, lane);
     const float y = tile_gemv<false>(Tpp, bvec + 32 * p, lo, hi);

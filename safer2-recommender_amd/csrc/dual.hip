@@ -376,7 +376,9 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   lds_barrier();
   mark(1);
 #if FRECSYS_CHOL_DF
-  chol_solve_df<TH, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip, a.prof);
+  // the MFMA-blocked diagonal factor where the register budget allows it
+  // (TH >= 6: one workgroup per CU anyway); TH = 3..5 keep their occupancy
+  chol_solve_df<TH, NW, (TH >= 6)>(tiles, bvec, xvec, part, flag, tid, a.debug_skip, a.prof);
 #else
   chol_solve_tiles<TH, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
 #endif

@@ -18,7 +18,7 @@ __global__ void __launch_bounds__(256) bench(unsigned long long* out, float* sin
     if (wave == 0) {
       for (int i = lane; i < 1024; i += 64) tile[i] = t2[i];
       wave_lds_sync();
-      diag_factor_inv(tile, lane);
+      diag_factor_inv<FRECSYS_DIAG_BLK != 0>(tile, lane);
     }
     lds_barrier();
   }

@@ -10,7 +10,7 @@ __global__ void run(const float* A, float* Linv, float* Lrow, int* ok) {
   const int lane = threadIdx.x;
   for (int i = lane; i < 1024; i += 64) tile[sw(i >> 5, i & 31)] = A[i];
   __syncthreads();
-  ok[0] = diag_factor_inv(tile, lane);
+  ok[0] = diag_factor_inv<FRECSYS_DIAG_BLK != 0>(tile, lane);
   __syncthreads();
   for (int i = lane; i < 1024; i += 64) Linv[i] = tile[sw(i >> 5, i & 31)];
 }
