@@ -403,34 +403,53 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
     }
     set_ver(ver + tidx(I, J), p + 1, lane);
   };
-  auto factor_y = [&](int p) {  // F(p), then Y(p) (b_p final: bver(p) = p)
+  auto factor = [&](int p) {  // F(p)
     float* Tpp = tiles + tidx(p, p) * 1024;
     if (!(debug_skip & 2)) {
       if (!diag_factor_inv<BLK>(Tpp, lane) && lane == 0) flag[0] = 1;
     }
     set_ver(ver + tidx(p, p), p + 1, lane);
-    const float y = tile_gemv<false>(Tpp, bvec + 32 * p, lo, hi);
+  };
+  auto ysolve = [&](int p) {  // Y(p): L_pp^-1 published, b_p final (bver(p) = p)
+    const float y = tile_gemv<false>(tiles + tidx(p, p) * 1024, bvec + 32 * p, lo, hi);
     wave_lds_sync();
     if (hi == 0) bvec[32 * p + lo] = y;
     set_ver(yver, p + 1, lane);
   };
+  // with 8 waves the forward substitution (Y, and B of the next block) runs
+  // on its own wave behind the chain instead of on it
+  constexpr bool YW = NW >= 8;
+  constexpr int W0 = YW ? 2 : 1;  // first worker wave
 
   if (wave == 0) {
     // ---- the critical chain (issue priority over the worker on its SIMD) ----
     __builtin_amdgcn_s_setprio(2);
 #pragma unroll 1
-    for (int p = -1; p + 1 < T; ++p) {  // one factor_y call site
+    for (int p = -1; p + 1 < T; ++p) {  // one factor call site
       if (p >= 0) {
         wait_ver(ver + tidx(p + 1, p), p);  // all of panel < p's updates
         trsm(p + 1, p);
-        bupd(p + 1, p);
+        if (!YW) bupd(p + 1, p);
         wait_ver(ver + tidx(p + 1, p + 1), p);
         update(p + 1, p + 1, p);
       }
-      factor_y(p + 1);
+      factor(p + 1);
+      if (!YW) ysolve(p + 1);
     }
     __builtin_amdgcn_s_setprio(0);
     if (prof && lane == 0) atomicAdd(prof + 5, clock64() - t0);
+  } else if (YW && wave == 1) {
+    // ---- the forward substitution along the chain ----
+#pragma unroll 1
+    for (int p = 0; p < T; ++p) {
+      wait_ver(ver + tidx(p, p), p + 1);  // F(p)
+      wait_ver(bver + p, p);             // b_p final
+      ysolve(p);
+      if (p + 1 < T) {
+        wait_ver(ver + tidx(p + 1, p), p + 1);  // S(p+1, p)
+        bupd(p + 1, p);
+      }
+    }
   } else {
     // ---- workers: the rest of each panel, round-robin ----
     int k = 0;
@@ -438,7 +457,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
     for (int p = 0; p + 1 < T; ++p) {
 #pragma unroll 1
       for (int I = p + 2; I < T; ++I, ++k) {  // S(I, p), B(I, p)
-        if (1 + k % (NW - 1) != wave) continue;
+        if (W0 + k % (NW - W0) != wave) continue;
         wait_ver(ver + tidx(p, p), p + 1);
         wait_ver(ver + tidx(I, p), p);
         trsm(I, p);
@@ -449,7 +468,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
       for (int J = p + 1; J < T; ++J) {  // U(I, J, p), column by column
 #pragma unroll 1
         for (int I = (J == p + 1 ? p + 2 : J); I < T; ++I, ++k) {
-          if (1 + k % (NW - 1) != wave) continue;
+          if (W0 + k % (NW - W0) != wave) continue;
           wait_ver(ver + tidx(I, p), p + 1);
           wait_ver(ver + tidx(J, p), p + 1);
           wait_ver(ver + tidx(I, J), p);
@@ -457,7 +476,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
         }
       }
     }
-    if (prof && lane == 0) atomicAdd(prof + 6, (clock64() - t0) / (NW - 1));
+    if (prof && lane == 0) atomicAdd(prof + 6, (clock64() - t0) / (NW - W0));
   }
   lds_barrier();
   if (prof && tid == 0) atomicAdd(prof + 7, clock64() - t0);
