@@ -131,6 +131,10 @@ struct frecsys_ctx {
   int dual_on = 1;
   int dual_max_h = 256;
   int dual_serial = 0;  // FRECSYS_DUAL_SERIAL=1: no stream overlap (profiling)
+  // FRECSYS_UNIT_BASIS=0: Householder basis even for a uniform M.  Not wired yet:
+  // the Cholesky-basis launch that would set DualArgs::unit_m does not exist,
+  // so the history-space path always uses the Householder basis.
+  int unit_basis = 1;
   // per-kernel event pairs, resolved after the call's final synchronisation
   struct Pending {
     std::string name;
@@ -516,6 +520,7 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H")) c->dual_max_h = atoi(v);
   if (const char* v = getenv("FRECSYS_DUAL_SERIAL")) c->dual_serial = atoi(v);
+  if (const char* v = getenv("FRECSYS_UNIT_BASIS")) c->unit_basis = atoi(v);
   if (const char* v = getenv("FRECSYS_SPLIT_ROWS")) c->split_rows = atoi(v);
   if (const char* v = getenv("FRECSYS_WIDE_WS_MB")) c->wide_ws_mb = std::max(1, atoi(v));
   c->dual_max_h = std::min(c->dual_max_h, 32 * kDualMaxTiles);

@@ -119,6 +119,14 @@ __global__ void __launch_bounds__(256) dual_ldl_kernel(DualArgs a) {
   // l_k = b_k / d_{k-1}, d_k = a_k - l_k b_k (a = mu*diag + lam, b = mu*sub);
   // position-blocked table: consecutive lanes write consecutive floats
   const int64_t pp = a.pos0 + p;
+  if (a.unit_m) {  // the Cholesky basis: mu*T + lam*I -> I
+    for (int k = 0; k < Dp; ++k) {
+      a.table[blk_t(pp, 0, k, Dp)] = 0.0f;
+      a.table[blk_t(pp, 1, k, Dp)] = 1.0f;
+      a.table[blk_t(pp, 2, k, Dp)] = 1.0f;
+    }
+    return;
+  }
   float r = 0.0f;
   bool ok = true;
   for (int k = 0; k < Dp; ++k) {

@@ -113,6 +113,7 @@ struct DualArgs {
   const float* entity_reg;
   const float* other_weight;
   unsigned long long* fail;
+  int unit_m;      // the basis is W = L^-T of M (launch_chol_basis): mu*T + lam*I -> I
   int debug_skip;  // ablation only: 1 SYRK, 2/4/8/16 Cholesky parts, 64 Y^T z, 128 recurrence
   unsigned long long* prof;  // diagnostics: per-phase cycle sums [16] (nullptr = off)
 };
