@@ -21,7 +21,7 @@ HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/dual.hip $(CSRC)/spectral.hip $(CSRC)/gram
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h $(CSRC)/chol.h include/frecsys_hip.h
 
-.PHONY: all lib oracle run_model model_dump clean
+.PHONY: all lib oracle run_model model_dump clean ablation
 all: lib oracle run_model model_dump
 lib: $(LIB)
 oracle: $(ORACLE)
@@ -51,3 +51,12 @@ $(MODELDUMP): tests/cpp/model_dump.cc $(FRECSYS_HDRS) include/frecsys_hip.h $(LI
 	@mkdir -p $(PKG)/bin
 	g++ $(CXXFLAGS) -o $@ tests/cpp/model_dump.cc -L$(PKG)/frecsys_hip -lfrecsys_hip \
 	    -Wl,-rpath,'$$ORIGIN/../frecsys_hip'
+
+# Profiling-only build with the FRECSYS_DEBUG_SKIP ablation masks compiled in
+# (the shipped library refuses the variable).  scripts/ab_bench.sh swaps it in.
+ABL_LIB := ab/libfrecsys_hip_ablation.so
+ablation: $(ABL_LIB)
+$(ABL_LIB): $(HIP_SRCS) $(HDRS)
+	@mkdir -p ab/obj
+	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) -DFRECSYS_ABLATION -c $$f -o ab/obj/$$(basename $$f .hip).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ ab/obj/*.o -lrccl

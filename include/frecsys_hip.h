@@ -229,6 +229,14 @@ int frecsys_timing_reset(frecsys_ctx* ctx);
  * sub[Dp]: T(k+1, k), sub[Dp-1] = 0); Dp = frecsys_padded_dim(dim).  No
  * reference counterpart. */
 int frecsys_debug_basis(frecsys_ctx* ctx, int32_t side, float* q, float* diag, float* sub);
+/* The two diagonal-block factorisations of the blocked Cholesky (the
+ * 32x32 pivot blocks of every solve): for each of n_tiles row-major 32x32
+ * SPD tiles a[t], linv[t] = L^-1 with L L^T = a[t] (lower; upper part 0),
+ * by the MFMA-blocked factor (blocked != 0) or the lane recurrence;
+ * ok[t] = 0 on a non-positive pivot.  No reference counterpart (Eigen's
+ * LLT inner kernel, ials.h:140). */
+int frecsys_debug_diag_factor(frecsys_ctx* ctx, int32_t blocked, int32_t n_tiles, const float* a,
+                              float* linv, int32_t* ok);
 
 #ifdef __cplusplus
 }

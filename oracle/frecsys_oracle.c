@@ -818,27 +818,39 @@ float oracle_safer2_weight(float loss, float xi, float bandwidth, int epan) {
   return 1 - gaussian_kernel_cdf(-r, bandwidth);
 }
 
-/* EvaluateQuantile, safer2.h:652-689.  Means accumulate in double. */
+/* EvaluateQuantile, safer2.h:652-689.  r = user_loss.array() - xi in float;
+ * each r.unaryExpr(lambda).mean() is Eigen's reduction of an expression
+ * without packet access (Redux.h DefaultTraversal): sequential float sum
+ * from the first element, divided by float(n). */
 static void evaluate_quantile(float xi, const float* loss, int64_t n, float alpha, float bw,
                               int epan, float* value, float* grad, float* H) {
-  double sc = 0, sk = 0, sl = 0;
+  float sc = 0, sk = 0, sl = 0;
   for (int64_t i = 0; i < n; ++i) {
     const float u = loss[i] - xi;
+    float c, k, l;
     if (epan) {
-      sc += epanechnikov_kernel_cdf(-u, bw);
-      sk += epanechnikov_kernel(-u, bw);
-      sl += epanechnikov_loss(u, bw, alpha);
+      c = epanechnikov_kernel_cdf(-u, bw);
+      k = epanechnikov_kernel(-u, bw);
+      l = epanechnikov_loss(u, bw, alpha);
     } else {
-      sc += gaussian_kernel_cdf(-u, bw);
-      sk += gaussian_kernel(-u, bw);
-      sl += gaussian_loss(u, bw, alpha);
+      c = gaussian_kernel_cdf(-u, bw);
+      k = gaussian_kernel(-u, bw);
+      l = gaussian_loss(u, bw, alpha);
+    }
+    if (i == 0) {
+      sc = c;
+      sk = k;
+      sl = l;
+    } else {
+      sc += c;
+      sk += k;
+      sl += l;
     }
   }
-  const float mc = (float)(sc / (double)n), mk = (float)(sk / (double)n),
-              ml = (float)(sl / (double)n);
-  *grad = (-(1 - alpha) + mc) / alpha;
-  *H = mk / alpha;
-  *value = ml / alpha;
+  const float fn = (float)n;
+  *grad = (-(1 - alpha) + sc / fn) / alpha;
+  *H = (sk / fn) / alpha;
+  *value = (sl / fn) / alpha;
 }
 
 /* ComputeXiDirection, safer2.h:692-712 (Armijo uses grad at the trial
@@ -872,6 +884,43 @@ float oracle_safer2_xi(const float* loss, int64_t n, float prev_xi, int iteratio
   return xi;
 }
 
+/* std::uniform_int_distribution<int>(0, range - 1)(mt19937) of libstdc++
+ * (GCC 11, bits/uniform_int_dist.h): the generator yields exactly 32 bits,
+ * so the draw is Lemire's nearly-divisionless reduction _S_nd with 64-bit
+ * products.  Checked against libstdc++ itself in tests/test_oracle.py. */
+uint32_t oracle_uniform_int(oracle_mt19937* g, uint32_t range) {
+  uint64_t product = (uint64_t)oracle_mt_next(g) * (uint64_t)range;
+  uint32_t low = (uint32_t)product;
+  if (low < range) {
+    const uint32_t threshold = (uint32_t)(-range) % range;
+    while (low < threshold) {
+      product = (uint64_t)oracle_mt_next(g) * (uint64_t)range;
+      low = (uint32_t)product;
+    }
+  }
+  return (uint32_t)(product >> 32);
+}
+
+/* ComputeXi, safer2.h:716-742, use_snr = true: every iteration draws
+ * int(N * sampling_ratio) user indices uniformly with replacement
+ * (:727-734) and takes the Newton/Armijo step on that sample (:735).  The
+ * reference seeds a fresh mt19937 from std::random_device per iteration;
+ * the build's --seed replaces that with one seeded generator (SURVEY
+ * App. A.7) that persists across calls, restated here as *g. */
+float oracle_safer2_xi_snr(const float* loss, int64_t n, float prev_xi, int iterations,
+                           float alpha, float bandwidth, int epan, float sampling_ratio,
+                           oracle_mt19937* g) {
+  float xi = prev_xi;
+  const int ns = (int)((float)n * sampling_ratio);
+  float* sample = (float*)malloc(sizeof(float) * (ns > 0 ? ns : 1));
+  for (int t = 0; t < iterations; ++t) {
+    for (int j = 0; j < ns; ++j) sample[j] = loss[oracle_uniform_int(g, (uint32_t)n)];
+    xi = xi + xi_direction(xi, sample, ns, alpha, bandwidth, epan);
+  }
+  free(sample);
+  return xi;
+}
+
 static int cmp_float_asc(const void* a, const void* b) {
   float x = *(const float*)a, y = *(const float*)b;
   return (x > y) - (x < y);
@@ -897,6 +946,7 @@ struct oracle_model {
   float *item_gramian, *G2;
   float *user_loss, *dual_weight, *hsize, *item_reg, *nu;
   float prev_xi;
+  oracle_mt19937 snr;
   const int64_t *u_ptr, *i_ptr;
   const int32_t *u_col, *i_col;
 };
@@ -919,6 +969,7 @@ oracle_model* oracle_model_create(const oracle_model_params* p, uint32_t seed) {
   for (int64_t u = 0; u < p->n_users; ++u) m->dual_weight[u] = p->alpha; /* safer2.h:56 */
   oracle_gramian(m->V, p->n_items, d, NULL, m->item_gramian, p->nthreads); /* :55 */
   m->prev_xi = 0.0f;
+  oracle_mt_seed(&m->snr, seed + 7919u);
   return m;
 }
 
@@ -965,10 +1016,55 @@ void oracle_model_get_state(const oracle_model* m, float* user_loss, float* dual
   if (xi) *xi = m->prev_xi;
 }
 
-static double mean_f(const float* x, int64_t n) {
-  double s = 0;
-  for (int64_t i = 0; i < n; ++i) s += x[i];
-  return s / (double)n;
+/* VectorXf::mean() of the reference (Eigen 3.4 Redux.h,
+ * LinearVectorizedTraversal, AVX-512 packets of 16 floats under
+ * -march=native): two packet accumulators, the predux<Packet16f> tree, the
+ * trailing scalars, then / float(n).  Same restatement as the product's
+ * include/frecsys/types.h detail::eigen_packet_sum. */
+static float eigen_packet_sum(const float* x, int64_t n) {
+  enum { P = 16 };
+  if (n <= 0) return 0.0f;
+  const int64_t aligned = n / P * P, aligned2 = n / (2 * P) * (2 * P);
+  if (aligned == 0) {
+    float r = x[0];
+    for (int64_t i = 1; i < n; ++i) r += x[i];
+    return r;
+  }
+  float p0[P], p1[P];
+  for (int k = 0; k < P; ++k) p0[k] = x[k];
+  if (aligned > P) {
+    for (int k = 0; k < P; ++k) p1[k] = x[P + k];
+    for (int64_t i = 2 * P; i < aligned2; i += 2 * P)
+      for (int k = 0; k < P; ++k) {
+        p0[k] += x[i + k];
+        p1[k] += x[i + P + k];
+      }
+    for (int k = 0; k < P; ++k) p0[k] += p1[k];
+    if (aligned > aligned2)
+      for (int k = 0; k < P; ++k) p0[k] += x[aligned2 + k];
+  }
+  float s8[8], s4[4];
+  for (int k = 0; k < 8; ++k) s8[k] = p0[k] + p0[k + 8];
+  for (int k = 0; k < 4; ++k) s4[k] = s8[k] + s8[k + 4];
+  const float t0 = s4[0] + s4[2], t1 = s4[1] + s4[3];
+  float r = t0 + t1;
+  for (int64_t i = aligned; i < n; ++i) r += x[i];
+  return r;
+}
+
+float oracle_mean(const float* x, int64_t n) {
+  return n > 0 ? eigen_packet_sum(x, n) / (float)n : 0.0f;
+}
+
+/* SAFER2 ComputeXi of the model: exact Newton, or SNR on the model's
+ * seeded sample stream (the product seeds it with seed + 7919). */
+static float model_xi(oracle_model* m, float prev) {
+  const oracle_model_params* p = &m->p;
+  if (p->use_snr)
+    return oracle_safer2_xi_snr(m->user_loss, p->n_users, prev, p->xi_iterations, p->alpha,
+                                p->bandwidth, p->use_epanechnikov, p->sampling_ratio, &m->snr);
+  return oracle_safer2_xi(m->user_loss, p->n_users, prev, p->xi_iterations, p->alpha,
+                          p->bandwidth, p->use_epanechnikov);
 }
 
 /* Initialize: safer2.h:819-838, erm_mf.h:573-587, cvar_mf.h:710-726. */
@@ -978,9 +1074,8 @@ void oracle_model_initialize(oracle_model* m) {
   oracle_user_loss(p->n_users, m->u_ptr, m->u_col, m->U, m->V, p->dim, m->item_gramian, p->w, 1,
                    m->user_loss, p->nthreads);
   if (p->model == 3) {
-    float prev = (float)mean_f(m->user_loss, p->n_users);
-    m->prev_xi = oracle_safer2_xi(m->user_loss, p->n_users, prev, p->xi_iterations, p->alpha,
-                                  p->bandwidth, p->use_epanechnikov);
+    float prev = oracle_mean(m->user_loss, p->n_users);
+    m->prev_xi = model_xi(m, prev);
   }
   for (int64_t u = 0; u < p->n_users; ++u) m->hsize[u] = (float)(m->u_ptr[u + 1] - m->u_ptr[u]);
   for (int64_t v = 0; v < p->n_items; ++v) {
@@ -1055,9 +1150,7 @@ int64_t oracle_model_train(oracle_model* m) {
     oracle_user_loss(p->n_users, m->u_ptr, m->u_col, m->U, m->V, d, m->item_gramian, p->w, 1,
                      m->user_loss, p->nthreads);
   }
-  if (p->model == 3)
-    m->prev_xi = oracle_safer2_xi(m->user_loss, p->n_users, m->prev_xi, p->xi_iterations,
-                                  p->alpha, p->bandwidth, p->use_epanechnikov);
+  if (p->model == 3) m->prev_xi = model_xi(m, m->prev_xi);
   return 0;
 }
 

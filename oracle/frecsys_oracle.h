@@ -124,6 +124,14 @@ void oracle_user_loss(int64_t n_users, const int64_t* row_ptr,
 float oracle_safer2_weight(float loss, float xi, float bandwidth, int epan);
 float oracle_safer2_xi(const float* loss, int64_t n, float prev_xi,
                        int iterations, float alpha, float bandwidth, int epan);
+/* use_snr: N*sampling_ratio indices per iteration from *g (see .c). */
+float oracle_safer2_xi_snr(const float* loss, int64_t n, float prev_xi, int iterations,
+                           float alpha, float bandwidth, int epan, float sampling_ratio,
+                           oracle_mt19937* g);
+/* libstdc++ uniform_int_distribution<int>(0, range-1) over mt19937. */
+uint32_t oracle_uniform_int(oracle_mt19937* g, uint32_t range);
+/* Eigen VectorXf::mean() restated (AVX-512 packet redux). */
+float oracle_mean(const float* x, int64_t n);
 /* CVaR-MF exact quantile (cvar_mf.h:582-595) */
 float oracle_cvar_xi(const float* loss, int64_t n, float alpha);
 
@@ -138,6 +146,8 @@ typedef struct {
   int xi_iterations, pd_iterations, use_epanechnikov;
   int quirk;
   int nthreads;
+  int use_snr;          /* SAFER2 sub-sampled Newton (safer2.h:724-737) */
+  float sampling_ratio;
 } oracle_model_params;
 
 oracle_model* oracle_model_create(const oracle_model_params* p,

@@ -28,7 +28,8 @@ class ModelParams(ctypes.Structure):
                 ("n_items", I64), ("reg", F), ("reg_exp", F), ("w", F), ("stdev", F),
                 ("alpha", F), ("bandwidth", F), ("stepsize", F), ("xi_iterations", ctypes.c_int),
                 ("pd_iterations", ctypes.c_int), ("use_epanechnikov", ctypes.c_int),
-                ("quirk", ctypes.c_int), ("nthreads", ctypes.c_int)]
+                ("quirk", ctypes.c_int), ("nthreads", ctypes.c_int), ("use_snr", ctypes.c_int),
+                ("sampling_ratio", F)]
 
 
 _lib = None
@@ -65,6 +66,9 @@ def lib():
                                      ctypes.c_int, P, P, P, ctypes.c_int]),
             "oracle_mt_seed": (None, [P, ctypes.c_uint32]),
             "oracle_mt_next": (ctypes.c_uint32, [P]),
+            "oracle_uniform_int": (ctypes.c_uint32, [P, ctypes.c_uint32]),
+            "oracle_mean": (F, [P, I64]),
+            "oracle_safer2_xi_snr": (F, [P, I64, F, ctypes.c_int, F, F, ctypes.c_int, F, P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -181,10 +185,10 @@ class Model:
 
     def __init__(self, model, dim, n_users, n_items, reg, w, stdev=0.1, alpha=0.3, reg_exp=1.0,
                  bandwidth=1.0, stepsize=0.1, xi_iterations=5, pd_iterations=1, epan=False,
-                 quirk=1, nthreads=0, seed=1):
+                 quirk=1, nthreads=0, seed=1, use_snr=False, sampling_ratio=0.1):
         self.p = ModelParams(model, dim, n_users, n_items, reg, reg_exp, w, stdev, alpha,
                              bandwidth, stepsize, xi_iterations, pd_iterations, 1 if epan else 0,
-                             quirk, nthreads)
+                             quirk, nthreads, 1 if use_snr else 0, sampling_ratio)
         self.h = lib().oracle_model_create(ctypes.byref(self.p), seed)
         self.dim, self.n_users, self.n_items = dim, n_users, n_items
         self._keep = []
@@ -242,3 +246,25 @@ def evaluate(Ueval, V, ex_ptr, ex_col, gt_ptr, gt_col, k_list=(5, 10, 20, 50, 10
     lib().oracle_evaluate(n, _p(Ueval), _p(V), V.shape[0], V.shape[1], _p(arrs[0]), _p(arrs[1]),
                           _p(arrs[2]), _p(arrs[3]), _p(ks), len(ks), _p(rec), _p(ndcg), nthreads)
     return rec, ndcg
+
+
+def mean(x):
+    """Eigen VectorXf::mean() restated (frecsys_oracle.c oracle_mean)."""
+    x = f32(x)
+    return float(lib().oracle_mean(_p(x), len(x)))
+
+
+def safer2_xi_snr(loss, prev_xi, iterations, alpha, bandwidth, epan, sampling_ratio, seed):
+    """SNR ComputeXi with a fresh generator seeded `seed`; returns xi."""
+    loss = f32(loss)
+    g = (ctypes.c_uint32 * 626)()
+    lib().oracle_mt_seed(g, seed)
+    return float(lib().oracle_safer2_xi_snr(_p(loss), len(loss), prev_xi, iterations, alpha,
+                                            bandwidth, 1 if epan else 0, sampling_ratio, g))
+
+
+def uniform_ints(seed, rng_range, count):
+    """libstdc++ uniform_int_distribution<int>(0, rng_range-1) draws from mt19937(seed)."""
+    g = (ctypes.c_uint32 * 626)()
+    lib().oracle_mt_seed(g, seed)
+    return [int(lib().oracle_uniform_int(g, rng_range)) for _ in range(count)]

@@ -131,10 +131,7 @@ struct frecsys_ctx {
   int dual_on = 1;
   int dual_max_h = 256;
   int dual_serial = 0;  // FRECSYS_DUAL_SERIAL=1: no stream overlap (profiling)
-  // FRECSYS_UNIT_BASIS=0: Householder basis even for a uniform M.  Not wired yet:
-  // the Cholesky-basis launch that would set DualArgs::unit_m does not exist,
-  // so the history-space path always uses the Householder basis.
-  int unit_basis = 1;
+  int debug_skip = 0;   // FRECSYS_DEBUG_SKIP ablation mask (-DFRECSYS_ABLATION builds only)
   // per-kernel event pairs, resolved after the call's final synchronisation
   struct Pending {
     std::string name;
@@ -330,7 +327,7 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
 // Row-range all-gather of a [rows x ld] float matrix (uneven per-rank
 // counts): every rank broadcasts its own range in place.
 int allgather_rows(frecsys_ctx* c, float* base, int side, int64_t ld) {
-  if (c->world == 1 || !c->comm) return FRECSYS_OK;  // external exchange: the caller's
+  if (!c->comm) return FRECSYS_OK;  // world 1 without RCCL, or external exchange: the caller's
   NCCL_TRY(c, ncclGroupStart());
   for (int r = 0; r < c->world; ++r) {
     const int64_t lo = c->bounds[side][r], hi = c->bounds[side][r + 1];
@@ -520,8 +517,18 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H")) c->dual_max_h = atoi(v);
   if (const char* v = getenv("FRECSYS_DUAL_SERIAL")) c->dual_serial = atoi(v);
-  if (const char* v = getenv("FRECSYS_UNIT_BASIS")) c->unit_basis = atoi(v);
   if (const char* v = getenv("FRECSYS_SPLIT_ROWS")) c->split_rows = atoi(v);
+  if (const char* v = getenv("FRECSYS_DEBUG_SKIP")) {
+#ifdef FRECSYS_ABLATION
+    c->debug_skip = atoi(v);
+#else
+    // a release build has no ablation masks: refuse rather than silently
+    // run the full work under a variable that claims to skip some
+    if (atoi(v) != 0)
+      return bail(fail(c, FRECSYS_ERR_INVALID,
+                       "FRECSYS_DEBUG_SKIP needs a -DFRECSYS_ABLATION build of libfrecsys_hip.so"));
+#endif
+  }
   if (const char* v = getenv("FRECSYS_WIDE_WS_MB")) c->wide_ws_mb = std::max(1, atoi(v));
   c->dual_max_h = std::min(c->dual_max_h, 32 * kDualMaxTiles);
   for (int s = 0; s < 2; ++s) {
@@ -624,7 +631,7 @@ int frecsys_comm_init(frecsys_ctx* c, int32_t world, int32_t rank, const uint8_t
   }
   c->world = world;
   c->rank = rank;
-  if (world > 1 && id) {
+  if (id) {  // a communicator at every world size (world 1: the exchange path still runs)
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
     NCCL_TRY(c, ncclCommInitRank(&c->comm, world, uid, rank));
@@ -779,7 +786,7 @@ int frecsys_gramian(frecsys_ctx* c, int32_t side, const float* weights, int32_t 
     HIP_TRY(c, launch_gramian(c->Dp, g, c->stream));
     t.stop();
   }
-  if (c->world > 1 && c->comm) {
+  if (c->comm) {
     ScopedTimer t(c, "allreduce");
     NCCL_TRY(c, ncclAllReduce(c->gram[side], c->gram[side], (size_t)c->Dp * c->Dp, ncclFloat,
                               ncclSum, c->comm, c->stream));
@@ -902,10 +909,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
   a.slabs = nullptr;
   a.work = nullptr;
   a.n_work = 0;
-  {
-    static const int dbg = getenv("FRECSYS_DEBUG_SKIP") ? atoi(getenv("FRECSYS_DEBUG_SKIP")) : 0;
-    a.debug_skip = dbg;
-  }
+  a.debug_skip = c->debug_skip;
   const unsigned long long none = ~0ull;
   HIP_TRY(c, hipMemcpyAsync(c->d_fail, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
   // Queue split: the queue is sorted by decreasing history, and h_eff (the
@@ -1038,7 +1042,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
     }
     t.stop();
   }
-  const bool collective = side < 2 && c->world > 1 && c->comm;
+  const bool collective = side < 2 && c->comm;
   if (collective) {
     // every rank takes the same retry / NOT_SPD decision below (the
     // smallest failing entity over all ranks), so the collectives of a
@@ -1047,7 +1051,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
   }
   unsigned long long f = none;
   HIP_TRY(c, hipMemcpyAsync(&f, c->d_fail, sizeof(f), hipMemcpyDeviceToHost, c->stream));
-  if (side < 2 && c->world > 1) {
+  if (side < 2 && (c->world > 1 || c->comm)) {
     ScopedTimer t(c, "allgather");
     rc = allgather_rows(c, c->emb[side], side, c->Dp);
     if (rc) return rc;
@@ -1123,7 +1127,7 @@ int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, fl
     t.stop();
   }
   if (host_out) {
-    if (side == 0 && c->world > 1) {
+    if (side == 0 && (c->world > 1 || c->comm)) {
       rc = allgather_rows(c, c->d_loss, 0, 1);
       if (rc) return rc;
     }
@@ -1379,6 +1383,30 @@ int frecsys_timing(const frecsys_ctx* c, const char* what, double* total_ms, int
   auto it = c->timers.find(what);
   if (total_ms) *total_ms = it == c->timers.end() ? 0.0 : it->second.total_ms;
   if (launches) *launches = it == c->timers.end() ? 0 : it->second.launches;
+  return FRECSYS_OK;
+}
+
+int frecsys_debug_diag_factor(frecsys_ctx* c, int32_t blocked, int32_t n_tiles, const float* a,
+                              float* linv, int32_t* ok) {
+  if (!c || n_tiles < 0 || (n_tiles && (!a || !linv || !ok)))
+    return fail(c, FRECSYS_ERR_INVALID, "debug_diag_factor: bad arguments");
+  if (n_tiles == 0) return FRECSYS_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  float *dA = nullptr, *dL = nullptr;
+  int* dok = nullptr;
+  const size_t bytes = sizeof(float) * 1024 * (size_t)n_tiles;
+  HIP_TRY(c, hipMalloc((void**)&dA, bytes));
+  HIP_TRY(c, hipMalloc((void**)&dL, bytes));
+  HIP_TRY(c, hipMalloc((void**)&dok, sizeof(int) * (size_t)n_tiles));
+  HIP_TRY(c, hipMemcpyAsync(dA, a, bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_debug_diag(dA, dL, dok, n_tiles, blocked ? 1 : 0, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(linv, dL, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(ok, dok, sizeof(int) * (size_t)n_tiles, hipMemcpyDeviceToHost,
+                            c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipFree(dA));
+  HIP_TRY(c, hipFree(dL));
+  HIP_TRY(c, hipFree(dok));
   return FRECSYS_OK;
 }
 

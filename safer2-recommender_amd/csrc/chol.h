@@ -207,7 +207,7 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
   static_assert(T - 1 < NW || T == 1, "back substitution needs one wave per tile");
   const int lane = tid & 63, lo = lane & 31, hi = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (wave == 0 && !(debug_skip & 2)) {
+  if (wave == 0 && !FRECSYS_SKIP(debug_skip, 2)) {
     if (!diag_factor_inv(tiles, lane) && lane == 0) flag[0] = 1;
   }
   lds_barrier();
@@ -216,7 +216,7 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
     const float* Tpp = tiles + tidx(p, p) * 1024;
     const int npan = T - 1 - p;
     // TRSM by MFMA: L_Ip = A_Ip (L_pp^-1)^T ; y_p = L_pp^-1 b_p
-    if (!(debug_skip & 4)) {
+    if (!FRECSYS_SKIP(debug_skip, 4)) {
       for (int t = wave; t < npan; t += NW) {
         float* Aip = tiles + tidx(p + 1 + t, p) * 1024;
         const f32x16 u = tile_pqT(Aip, Tpp, lo, hi);
@@ -248,16 +248,16 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
       if (wave == 0) {
         float* A11 = tiles + tidx(p + 1, p + 1) * 1024;
         const float* L1 = tiles + tidx(p + 1, p) * 1024;
-        if (!(debug_skip & 8)) {
+        if (!FRECSYS_SKIP(debug_skip, 8)) {
           const f32x16 u = tile_pqT(L1, L1, lo, hi);
 #pragma unroll
           for (int q = 0; q < 16; ++q) A11[sw(acc_row(q, hi), lo)] -= u[q];
         }
-        if (!(debug_skip & 2)) {
+        if (!FRECSYS_SKIP(debug_skip, 2)) {
           if (!diag_factor_inv(A11, lane) && lane == 0) flag[0] = 1;
         }
       } else {
-        for (int tt = wave; tt < ntr && !(debug_skip & 8); tt += NW - 1) {
+        for (int tt = wave; tt < ntr && !FRECSYS_SKIP(debug_skip, 8); tt += NW - 1) {
           int Ir = 0;
           while ((Ir + 1) * (Ir + 2) / 2 <= tt) ++Ir;
           const int Jr = tt - Ir * (Ir + 1) / 2;
@@ -276,7 +276,7 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
   // r_p = y_p - sum_{q>p} L_qp^T x_q   (one wave per q, partials in LDS)
   // x_p = (L_pp^-1)^T r_p
 #pragma unroll 1
-  for (int p = T - 1; p >= 0 && !(debug_skip & 16); --p) {
+  for (int p = T - 1; p >= 0 && !FRECSYS_SKIP(debug_skip, 16); --p) {
     const int nq = T - 1 - p;  // < NW: one q per wave
     if (wave < nq) {
       const int q = p + 1 + wave;
@@ -381,7 +381,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
 
   auto trsm = [&](int I, int p) {  // S(I, p)
     float* Aip = tiles + tidx(I, p) * 1024;
-    if (!(debug_skip & 4)) {
+    if (!FRECSYS_SKIP(debug_skip, 4)) {
       const f32x16 u = tile_pqT(Aip, tiles + tidx(p, p) * 1024, lo, hi);
 #pragma unroll
       for (int q = 0; q < 16; ++q) Aip[sw(acc_row(q, hi), lo)] = u[q];
@@ -396,7 +396,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   };
   auto update = [&](int I, int J, int p) {  // U(I, J, p)
     float* Aij = tiles + tidx(I, J) * 1024;
-    if (!(debug_skip & 8)) {
+    if (!FRECSYS_SKIP(debug_skip, 8)) {
       const f32x16 u = tile_pqT(tiles + tidx(I, p) * 1024, tiles + tidx(J, p) * 1024, lo, hi);
 #pragma unroll
       for (int q = 0; q < 16; ++q) Aij[sw(acc_row(q, hi), lo)] -= u[q];
@@ -405,7 +405,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   };
   auto factor = [&](int p) {  // F(p)
     float* Tpp = tiles + tidx(p, p) * 1024;
-    if (!(debug_skip & 2)) {
+    if (!FRECSYS_SKIP(debug_skip, 2)) {
       if (!diag_factor_inv<BLK>(Tpp, lane) && lane == 0) flag[0] = 1;
     }
     set_ver(ver + tidx(p, p), p + 1, lane);

@@ -4,6 +4,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Ablation masks (FRECSYS_DEBUG_SKIP) skip whole phases of the solve kernels
+// for profiling.  They exist only in builds made with -DFRECSYS_ABLATION;
+// in the shipped library every FRECSYS_SKIP(...) is the constant 0 and the
+// skipped branches are compiled out.
+#ifdef FRECSYS_ABLATION
+#define FRECSYS_SKIP(mask, bit) ((mask) & (bit))
+#else
+#define FRECSYS_SKIP(mask, bit) 0
+#endif
+
 namespace frecsys_hip {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));

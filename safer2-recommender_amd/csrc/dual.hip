@@ -119,14 +119,6 @@ __global__ void __launch_bounds__(256) dual_ldl_kernel(DualArgs a) {
   // l_k = b_k / d_{k-1}, d_k = a_k - l_k b_k (a = mu*diag + lam, b = mu*sub);
   // position-blocked table: consecutive lanes write consecutive floats
   const int64_t pp = a.pos0 + p;
-  if (a.unit_m) {  // the Cholesky basis: mu*T + lam*I -> I
-    for (int k = 0; k < Dp; ++k) {
-      a.table[blk_t(pp, 0, k, Dp)] = 0.0f;
-      a.table[blk_t(pp, 1, k, Dp)] = 1.0f;
-      a.table[blk_t(pp, 2, k, Dp)] = 1.0f;
-    }
-    return;
-  }
   float r = 0.0f;
   bool ok = true;
   for (int k = 0; k < Dp; ++k) {
@@ -230,8 +222,8 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   {  // l_k and D^-1/2 from the entity's table row
     const int64_t pp = a.pos0 + blockIdx.x;
     for (int k = tid; k < Dp; k += NTHR) {
-      lsub[k] = (a.debug_skip & 256) ? 0.5f : a.table[blk_t(pp, 0, k, Dp)];
-      dsq[k] = (a.debug_skip & 256) ? 0.5f : a.table[blk_t(pp, 1, k, Dp)];
+      lsub[k] = FRECSYS_SKIP(a.debug_skip, 256) ? 0.5f : a.table[blk_t(pp, 0, k, Dp)];
+      dsq[k] = FRECSYS_SKIP(a.debug_skip, 256) ? 0.5f : a.table[blk_t(pp, 1, k, Dp)];
     }
   }
   lds_barrier();
@@ -247,7 +239,7 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
       if ((HP * 8) % NTHR == 0 || s < HP * 8) {
         const int r = s >> 3, c4 = s & 7;
         const int id = ids[r];
-        if (id >= 0 && !(a.debug_skip & 32))
+        if (id >= 0 && !FRECSYS_SKIP(a.debug_skip, 32))
           regs[q] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)id * Dp + 32 * c + 4 * c4);
       }
     }
@@ -293,7 +285,7 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   // slab c: in LDS stage c&1; slab c+1 in the other register set
   auto slab_step = [&](int c, float4 (&mine)[NQ], float4 (&next)[NQ]) {
     if (c + 2 < NC) load_slab(c + 2, mine);
-    if (tid < HP && !(a.debug_skip & 128)) {
+    if (tid < HP && !FRECSYS_SKIP(a.debug_skip, 128)) {
       const float* yrow = stage + ((c & 1) % C::NSTAGE) * C::STG + tid * SROW;
       float y[BF ? 1 : 32];
       if constexpr (!BF) {
@@ -328,7 +320,7 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
       carry = z;
     }
     lds_barrier();
-    if (!(a.debug_skip & 1)) {
+    if (!FRECSYS_SKIP(a.debug_skip, 1)) {
       if constexpr (BF) {
         const bf16x8* zb = reinterpret_cast<const bf16x8*>(zs);
 #pragma unroll
@@ -398,7 +390,7 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
     const int c4 = tid % D4, g = tid / D4;
     float* red = tiles;  // the S tiles are dead after the solve
     float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (g < R && !(a.debug_skip & 64)) {
+    if (g < R && !FRECSYS_SKIP(a.debug_skip, 64)) {
       for (int j0 = g; j0 < ntot; j0 += 8 * R) {
         float4 rv[8];
         float wv[8];
@@ -457,7 +449,7 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
 #pragma unroll
   for (int p = 0; p < T; ++p) {
     float* Tpp = tiles + tidx(p, p) * 1024;
-    if (!(debug_skip & 2) && !diag_factor_inv(Tpp, lane) && lane == 0) flag[0] = 1;
+    if (!FRECSYS_SKIP(debug_skip, 2) && !diag_factor_inv(Tpp, lane) && lane == 0) flag[0] = 1;
     wave_sync();
     // y_p = L_pp^-1 b_p  (lane lo, both halves compute, half 0 keeps it)
     float yp = 0.0f;
@@ -693,7 +685,7 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   for (int cg = 0; 256 * cg < Dp; ++cg) {
   const int c4 = 4 * lane + 256 * cg;
   float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (c4 < Dp && !(a.debug_skip & 64)) {
+  if (c4 < Dp && !FRECSYS_SKIP(a.debug_skip, 64)) {
     for (int j0 = 0; j0 < ntot; j0 += 8) {
       float4 rv[8];
       float wv[8];
@@ -782,8 +774,8 @@ hipError_t launch_dual(int tiles, const DualArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
   if (a.Dp < 64 || a.Dp > kMaxDp || (a.Dp & 31)) return hipErrorInvalidValue;
   switch (tiles) {
-    case 1: return a.debug_skip & 512 ? launch_dual_t<1>(a, s) : launch_wave_t<1>(a, s);
-    case 2: return a.debug_skip & 512 ? launch_dual_t<2>(a, s) : launch_wave_t<2>(a, s);
+    case 1: return FRECSYS_SKIP(a.debug_skip, 512) ? launch_dual_t<1>(a, s) : launch_wave_t<1>(a, s);
+    case 2: return FRECSYS_SKIP(a.debug_skip, 512) ? launch_dual_t<2>(a, s) : launch_wave_t<2>(a, s);
     case 3: return launch_dual_t<3>(a, s);
     case 4: return launch_dual_t<4>(a, s);
     case 5: return launch_dual_t<5>(a, s);

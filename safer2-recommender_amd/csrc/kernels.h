@@ -113,7 +113,6 @@ struct DualArgs {
   const float* entity_reg;
   const float* other_weight;
   unsigned long long* fail;
-  int unit_m;      // the basis is W = L^-T of M (launch_chol_basis): mu*T + lam*I -> I
   int debug_skip;  // ablation only: 1 SYRK, 2/4/8/16 Cholesky parts, 64 Y^T z, 128 recurrence
   unsigned long long* prof;  // diagnostics: per-phase cycle sums [16] (nullptr = off)
 };
@@ -122,6 +121,9 @@ struct DualArgs {
 constexpr int kDualMaxTiles = 8;
 
 hipError_t launch_solve(int Dp, const SolveArgs& a, hipStream_t s);
+// Diagnostics: n 32x32 tiles (row-major) -> L^-1 of each (blk: the
+// MFMA-blocked diagonal factor, else the lane recurrence), ok[n].
+hipError_t launch_debug_diag(const float* A, float* Linv, int* ok, int n, int blk, hipStream_t s);
 // Partial SYRKs of the split entities (a.work[0..n_work)) into a.slabs.
 hipError_t launch_split_syrk(int Dp, const SolveArgs& a, hipStream_t s);
 size_t split_slab_floats(int Dp);

@@ -410,7 +410,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
             for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(f[hh][p]));
       };
       const bf16x8* st = reinterpret_cast<const bf16x8*>(stage) + buf * C::GRAN;
-      if (!(a.debug_skip & 1)) {
+      if (!FRECSYS_SKIP(a.debug_skip, 1)) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           // tiles every wave has: no branch, one basic block with the splits
@@ -459,7 +459,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
       const int slot = c % kRing;
       // tile-outer, row-pair-inner: one wave-uniform branch per tile and the
       // operand reads free to run ahead of the MFMAs
-      if (!(a.debug_skip & 1)) {
+      if (!FRECSYS_SKIP(a.debug_skip, 1)) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           if (valid[m]) {
@@ -773,6 +773,31 @@ hipError_t launch_split_syrk(int Dp, const SolveArgs& a, hipStream_t s) {
 size_t split_slab_floats(int Dp) {
   const int T = Dp / 32;
   return (size_t)T * (T + 1) / 2 * 1024 + Dp;
+}
+
+// Diagnostics (frecsys_debug_diag_factor): one wave per 32x32 tile, the
+// tile factored + inverted in LDS by the lane recurrence (blk = 0,
+// diag_factor_inv_lds) or the MFMA-blocked factor (blk = 1,
+// diag_factor_inv_blk) -- the two diagonal-block routines of chol.h.
+__global__ void __launch_bounds__(64)
+    debug_diag_kernel(const float* __restrict__ A, float* __restrict__ Linv, int* __restrict__ ok,
+                      int blk) {
+  __shared__ __attribute__((aligned(16))) float tile[1024];
+  const int lane = threadIdx.x;
+  const float* a = A + (int64_t)blockIdx.x * 1024;
+  for (int i = lane; i < 1024; i += 64) tile[sw(i >> 5, i & 31)] = a[i];
+  __syncthreads();
+  const bool good = blk ? diag_factor_inv_blk((lds_float*)tile, lane)
+                        : diag_factor_inv_lds((lds_float*)tile, lane);
+  __syncthreads();
+  for (int i = lane; i < 1024; i += 64) Linv[(int64_t)blockIdx.x * 1024 + i] = tile[sw(i >> 5, i & 31)];
+  if (lane == 0) ok[blockIdx.x] = good ? 1 : 0;
+}
+
+hipError_t launch_debug_diag(const float* A, float* Linv, int* ok, int n, int blk, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(debug_diag_kernel, dim3((unsigned)n), dim3(64), 0, s, A, Linv, ok, blk);
+  return hipGetLastError();
 }
 
 }  // namespace frecsys_hip

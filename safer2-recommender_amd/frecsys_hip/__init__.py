@@ -35,7 +35,7 @@ EXPORTS = (
     "frecsys_gramian", "frecsys_set_gramian", "frecsys_solve_side", "frecsys_user_loss",
     "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset", "frecsys_debug_basis",
     "frecsys_eval_topk", "frecsys_train_stats", "frecsys_pp_set_rating_index",
-    "frecsys_pp_predict", "frecsys_pp_step",
+    "frecsys_pp_predict", "frecsys_pp_step", "frecsys_debug_diag_factor",
 )
 
 
@@ -97,6 +97,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, P]),
         "frecsys_timing_reset": (ctypes.c_int, [P]),
         "frecsys_debug_basis": (ctypes.c_int, [P, I32, P, P, P]),
+        "frecsys_debug_diag_factor": (ctypes.c_int, [P, I32, I32, P, P, P]),
         "frecsys_eval_topk": (ctypes.c_int, [P, I32, P]),
         "frecsys_train_stats": (ctypes.c_int, [P, P, P, P, P]),
         "frecsys_pp_set_rating_index": (ctypes.c_int, [P, I32, P]),
@@ -303,6 +304,15 @@ class Context:
         self._check(self.lib.frecsys_train_stats(self.h, ctypes.byref(obs), ctypes.byref(unobs),
                                                  _ptr(un), _ptr(vn)))
         return obs.value, unobs.value, un, vn
+
+    def debug_diag_factor(self, tiles: np.ndarray, blocked: bool):
+        """L^-1 of each 32x32 SPD tile (diagnostic): (linv [n,32,32], ok [n])."""
+        a = np.ascontiguousarray(tiles, dtype=np.float32).reshape(-1, 32, 32)
+        out = np.zeros_like(a)
+        ok = np.zeros(len(a), dtype=np.int32)
+        self._check(self.lib.frecsys_debug_diag_factor(self.h, 1 if blocked else 0, len(a),
+                                                       _ptr(a), _ptr(out), _ptr(ok)))
+        return out, ok
 
     def debug_basis(self, side: int):
         """(Q, diag, sub) with G[side] = Q T Q^T (diagnostic, Dp >= 64)."""

@@ -60,24 +60,38 @@ struct Smoother {
   float alpha, bandwidth;
   bool epan;
   // EvaluateQuantile (safer2.h:652-689): value, gradient, Hessian of the
-  // smoothed quantile objective at xi; means accumulated in double.
+  // smoothed quantile objective at xi.  r = loss - xi is formed in float,
+  // and each `r.unaryExpr(lambda).mean()` is Eigen's reduction of an
+  // expression without packet access (Redux.h DefaultTraversal): a
+  // sequential float sum from the first element, then / float(n).
   std::tuple<float, float, float> Evaluate(float xi, const float* loss, int64_t n) const {
-    double sc = 0, sk = 0, sl = 0;
+    float sc = 0, sk = 0, sl = 0;
     for (int64_t i = 0; i < n; ++i) {
       const float u = loss[i] - xi;
+      float c, k, l;
       if (epan) {
-        sc += epanechnikov_kernel_cdf(-u, bandwidth);
-        sk += epanechnikov_kernel(-u, bandwidth);
-        sl += epanechnikov_loss(u, bandwidth, alpha);
+        c = epanechnikov_kernel_cdf(-u, bandwidth);
+        k = epanechnikov_kernel(-u, bandwidth);
+        l = epanechnikov_loss(u, bandwidth, alpha);
       } else {
-        sc += gaussian_kernel_cdf(-u, bandwidth);
-        sk += gaussian_kernel(-u, bandwidth);
-        sl += gaussian_loss(u, bandwidth, alpha);
+        c = gaussian_kernel_cdf(-u, bandwidth);
+        k = gaussian_kernel(-u, bandwidth);
+        l = gaussian_loss(u, bandwidth, alpha);
+      }
+      if (i == 0) {
+        sc = c;
+        sk = k;
+        sl = l;
+      } else {
+        sc += c;
+        sk += k;
+        sl += l;
       }
     }
-    const float grad = (-(1 - alpha) + (float)(sc / (double)n)) / alpha;
-    const float H = (float)(sk / (double)n) / alpha;
-    const float value = (float)(sl / (double)n) / alpha;
+    const float fn = (float)n;
+    const float grad = (-(1 - alpha) + sc / fn) / alpha;
+    const float H = (sk / fn) / alpha;
+    const float value = (sl / fn) / alpha;
     return {value, grad, H};
   }
   // ComputeXiDirection (safer2.h:692-712): Newton step with Armijo

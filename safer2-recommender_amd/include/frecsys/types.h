@@ -14,10 +14,56 @@
 #include <cstdint>
 #include <numeric>
 #include <unordered_map>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
 namespace frecsys {
+
+namespace detail {
+
+// Eigen 3.4 Redux.h, LinearVectorizedTraversal / NoUnrolling: the sum of a
+// plain (packet-accessible, aligned) float vector as the reference's
+// -march=native build computes it on an AVX-512 host (Packet16f):
+// packet accumulators p0 = x[0:16), p1 = x[16:32), then pairs of packets
+// added into p0 and p1 alternately, p0 += p1, one more packet if the aligned
+// part has an odd packet count, the horizontal reduction of
+// predux<Packet16f> (AVX512DQ: 8 + 8 -> 4 + 4 -> {0+2, 1+3} -> sum), then
+// the trailing scalars one by one.  Vectors shorter than one packet sum
+// sequentially.  (An AVX2 host would use 8-float packets: the same value up
+// to fp32 rounding.)
+inline float eigen_packet_sum(const float* x, int64_t n) {
+  constexpr int P = 16;
+  if (n <= 0) return 0.0f;
+  const int64_t aligned = n / P * P, aligned2 = n / (2 * P) * (2 * P);
+  if (aligned == 0) {
+    float r = x[0];
+    for (int64_t i = 1; i < n; ++i) r += x[i];
+    return r;
+  }
+  float p0[P], p1[P];
+  for (int k = 0; k < P; ++k) p0[k] = x[k];
+  if (aligned > P) {
+    for (int k = 0; k < P; ++k) p1[k] = x[P + k];
+    for (int64_t i = 2 * P; i < aligned2; i += 2 * P)
+      for (int k = 0; k < P; ++k) {
+        p0[k] += x[i + k];
+        p1[k] += x[i + P + k];
+      }
+    for (int k = 0; k < P; ++k) p0[k] += p1[k];
+    if (aligned > aligned2)
+      for (int k = 0; k < P; ++k) p0[k] += x[aligned2 + k];
+  }
+  float s8[8], s4[4];
+  for (int k = 0; k < 8; ++k) s8[k] = p0[k] + p0[k + 8];
+  for (int k = 0; k < 4; ++k) s4[k] = s8[k] + s8[k + 4];
+  const float t0 = s4[0] + s4[2], t1 = s4[1] + s4[3];
+  float r = t0 + t1;
+  for (int64_t i = aligned; i < n; ++i) r += x[i];
+  return r;
+}
+
+}  // namespace detail
 
 template <typename T>
 class DenseVector {
@@ -43,14 +89,19 @@ class DenseVector {
   const T& operator()(int64_t i) const { return v_[(size_t)i]; }
   T& operator[](int64_t i) { return v_[(size_t)i]; }
   const T& operator[](int64_t i) const { return v_[(size_t)i]; }
-  // Sum in double, returned in T (Eigen sums in T with SIMD partials; the
-  // double accumulation is the more accurate restatement).
+  // sum() / mean() restate Eigen's float reductions (detail::eigen_packet_sum
+  // below); other element types sum in double.
   T sum() const {
-    double s = 0.0;
-    for (const T& x : v_) s += (double)x;
-    return (T)s;
+    if constexpr (std::is_same<T, float>::value) {
+      return detail::eigen_packet_sum(v_.data(), (int64_t)v_.size());
+    } else {
+      double s = 0.0;
+      for (const T& x : v_) s += (double)x;
+      return (T)s;
+    }
   }
-  T mean() const { return v_.empty() ? T(0) : (T)(sumd() / (double)v_.size()); }
+  // Eigen DenseBase::mean(): sum() / T(size()), in T.
+  T mean() const { return v_.empty() ? T(0) : sum() / (T)v_.size(); }
   double sumd() const {
     double s = 0.0;
     for (const T& x : v_) s += (double)x;

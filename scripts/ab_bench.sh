@@ -5,6 +5,10 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
+# the masks exist only in the ablation build (make ablation); swap it in
+LIB=safer2-recommender_amd/frecsys_hip/libfrecsys_hip.so
+cp $LIB /tmp/libfrecsys_hip.release.so && cp ab/libfrecsys_hip_ablation.so $LIB || exit 9
+trap 'cp /tmp/libfrecsys_hip.release.so $LIB' EXIT
 OUT=gpurun_out/$1
 shift
 mkdir -p $OUT

@@ -33,35 +33,55 @@ def ml1m():
     return tr, vt, ve
 
 
-def make_quirk_data(seed=7, n_users=700, n_items=400, hot_items=(3, 11, 57, 200, 399),
-                    hot_frac=(0.40, 0.19, 0.29, 0.186, 0.5), idle_user=5, idle_item=9):
+def make_quirk_data(seed=7, n_users=700, n_items=400,
+                    hot_items=(3, 11, 57, 200, 399, 77, 123, 250, 260, 300),
+                    hot_frac=(0.40, 0.19, 0.29, 0.186, 0.5, 0.25, 0.34, 0.16, 0.115, 0.3658),
+                    idle_user=5, idle_item=9):
     """Small interaction set that hits the reference's edge cases: user
-    histories of length 1 / 5 / 128 / 129 / 200 / 300, item histories above
-    128 with a non-zero remainder mod 128 (ProjectV tail quirk), exactly 256,
-    one idle user and one idle item (rows with no history).  Returns
+    histories of length 1 / 5 / 128 / 129 / 170 / 200 / 250 / 300, item
+    histories above 128 with a non-zero remainder mod 128 (ProjectV tail
+    quirk), exactly 256, every history-space bucket (32 (t-1) < h <= 32 t,
+    t = 1..8) on both sides, one idle user and one idle item (rows with no
+    history).  Hot item k is in the histories of exactly round(hot_frac[k] *
+    n_users) users (drawn among users with room for it; no other user
+    draws it).  Returns
     (n_users, n_items, up, uc, ip, ic)."""
     rng = np.random.default_rng(seed)
-    fixed = {0: 1, 1: 5, 2: 128, 3: 129, 4: 200, 6: 300}
+    hot_rng = np.random.default_rng(seed + 1000)
+    fixed = {0: 1, 1: 5, 2: 128, 3: 129, 4: 200, 6: 300, 7: 170, 8: 250}
+    hs = {}
+    for u in range(n_users):
+        draw = int(np.clip(rng.lognormal(3.0, 0.7), 2, 150))
+        if u != idle_user:
+            hs[u] = fixed.get(u, draw)
+    hot = [int(h) for h in np.array(hot_items) % n_items]
+    pairs = list(zip(hot, hot_frac))
+    members = {u: [] for u in hs}
+    room = {u: min(hs[u], n_items - 1) for u in hs}
+    for it, fr in pairs:
+        if it == idle_item:
+            continue
+        cand = np.array([u for u in hs if room[u] > 0])
+        k = min(len(cand), int(round(fr * n_users)))
+        for u in hot_rng.choice(cand, k, replace=False):
+            members[int(u)].append(it)
+            room[int(u)] -= 1
     users, items = [], []
-    hot = np.array(hot_items) % n_items
     for u in range(n_users):
         if u == idle_user:
             continue
-        h = fixed.get(u, int(np.clip(rng.lognormal(3.0, 0.7), 2, 150)))
-        chosen = set()
-        for it, fr in zip(hot, hot_frac):
-            if rng.random() < fr and len(chosen) < h:
-                chosen.add(int(it))
-        pool = rng.permutation(n_items)
-        for it in pool:
+        h = hs[u]
+        chosen = list(dict.fromkeys(members[u]))
+        seen = set(chosen) | set(hot)  # hot items only through their members
+        for it in rng.permutation(n_items):
             if len(chosen) >= h:
                 break
-            if it != idle_item:
-                chosen.add(int(it))
-        lst = list(chosen)
-        rng.shuffle(lst)
-        users += [u] * len(lst)
-        items += lst
+            if it != idle_item and int(it) not in seen:
+                chosen.append(int(it))
+                seen.add(int(it))
+        rng.shuffle(chosen)
+        users += [u] * len(chosen)
+        items += chosen
     users = np.array(users, np.int64)
     items = np.array(items, np.int64)
     from frecsys_hip.data import _csr_from_pairs

@@ -20,7 +20,7 @@ int main(int argc, char** argv) {
   if (argc < 13) {
     fprintf(stderr,
             "usage: model_dump model dim epochs seed train.csv out.bin reg w alpha bandwidth "
-            "stepsize epan [test_tr test_te]\n");
+            "stepsize epan [use_snr sampling_ratio [test_tr test_te]]\n");
     return 2;
   }
   const std::string model = argv[1];
@@ -31,6 +31,8 @@ int main(int argc, char** argv) {
   const float reg = atof(argv[7]), w = atof(argv[8]), alpha = atof(argv[9]),
               bw = atof(argv[10]), eta = atof(argv[11]);
   const bool epan = atoi(argv[12]) != 0;
+  const bool use_snr = argc >= 15 && atoi(argv[13]) != 0;
+  const float sampling_ratio = argc >= 15 ? (float)atof(argv[14]) : 0.1f;
   frecsys::DeviceOptions o;
   o.seed = seed;
   const int nu = train.max_user() + 1, ni = train.max_item() + 1;
@@ -41,8 +43,8 @@ int main(int argc, char** argv) {
   if (model == "ials") {
     m = new frecsys::IALSRecommender(dim, nu, ni, reg, 1.0f, w, 0.1f, alpha, false, 1e-10, 100, o);
   } else if (model == "safer2") {
-    s2 = new frecsys::SAFER2Recommender(dim, nu, ni, reg, w, bw, alpha, 0.1f, 5, 1, epan, false,
-                                        0.1f, false, 1e-10, 100, o);
+    s2 = new frecsys::SAFER2Recommender(dim, nu, ni, reg, w, bw, alpha, 0.1f, 5, 1, epan, use_snr,
+                                        sampling_ratio, false, 1e-10, 100, o);
     m = s2;
   } else if (model == "erm_mf") {
     erm = new frecsys::ERMMFRecommender(dim, nu, ni, reg, w, 0.1f, alpha, false, 1e-10, 100, o);
@@ -64,8 +66,8 @@ int main(int argc, char** argv) {
     mean_w.push_back(s2 ? s2->GetMeanWeight() : erm ? erm->GetMeanWeight()
                                                      : cv ? cv->GetMeanWeight() : 0.0f);
   }
-  if (argc >= 15) {
-    frecsys::Dataset tr(argv[13]), te(argv[14]);
+  if (argc >= 17) {
+    frecsys::Dataset tr(argv[15]), te(argv[16]);
     frecsys::VectorXi k(5);
     k << 5, 10, 20, 50, 100;
     frecsys::VectorXf a(9);

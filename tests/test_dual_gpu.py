@@ -174,3 +174,38 @@ def test_eval_side_dual(monkeypatch, ml1m):
     ctx.solve_side(fh.SIDE_EVAL, fh.KIND_IALS, 0.003, 0.1)
     Uo, rc = O.step(ep, ec, V0, O.gramian(V0), 0, 0.003, 0.1)
     assert rel_rows(ctx.get_embeddings(fh.SIDE_EVAL), Uo).max() < TOL_ROW
+
+
+def _buckets(h):
+    """History-space bucket t (32 (t-1) < h <= 32 t) per entity, as the host
+    queue split in capi.hip solve_side_impl assigns them (iALS: h_eff = h)."""
+    b = np.ceil(np.asarray(h) / 32.0).astype(int)
+    return [int(((b == t) & (np.asarray(h) > 0)).sum()) for t in range(1, 9)]
+
+
+def test_every_bucket_filled_and_solved(quirk_data, monkeypatch):
+    """The default fixture puts entities in every history-space bucket
+    TH = 1..8 on both sides (TH = 6 and 8 run the MFMA-blocked diagonal
+    factor, TH <= 2 the wave-per-entity kernel) and some in d space; one
+    iALS epoch over it matches the oracle on every row."""
+    nu, ni, up, uc, ip, ic = quirk_data
+    hu, hi = np.diff(up), np.diff(ip)
+    assert all(c > 0 for c in _buckets(hu)), _buckets(hu)
+    assert all(c > 0 for c in _buckets(hi)), _buckets(hi)
+    assert (hu > 256).any() and (hi > 256).any()
+    dim = 256
+    ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+    reg, w = 0.003, 0.1
+    ctx.gramian(fh.SIDE_ITEM)
+    ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, reg, w)
+    assert ctx.timing("solve_user.hspace")[1] == 1 and ctx.timing("solve_user.dspace")[1] == 1
+    Uo, rc = O.step(up, uc, V, O.gramian(V), 0, reg, w, out=U.copy())
+    assert rc == 0
+    assert rel_rows(ctx.get_embeddings(fh.SIDE_USER), Uo).max() < TOL_ROW
+    ctx.set_embeddings(fh.SIDE_USER, Uo)
+    ctx.gramian(fh.SIDE_USER)
+    ctx.solve_side(fh.SIDE_ITEM, fh.KIND_IALS, reg, w)
+    assert ctx.timing("solve_item.hspace")[1] == 1 and ctx.timing("solve_item.dspace")[1] == 1
+    Vo, rc = O.step(ip, ic, Uo, O.gramian(Uo), 0, reg, w, out=V.copy())
+    assert rc == 0
+    assert rel_rows(ctx.get_embeddings(fh.SIDE_ITEM), Vo).max() < TOL_ROW

@@ -45,13 +45,31 @@ def _read_dump(path, epochs, with_ndcg):
 
 
 CASES = {
-    # model: (oracle id, reg, w, alpha, bandwidth, stepsize, epan)
-    "ials": (O.MODEL_IALS, 0.003, 0.1, 0.3, 1.0, 0.1, 0),
-    "erm_mf": (O.MODEL_ERM, 0.005, 0.004, 0.3, 1.0, 0.1, 0),
-    "cvar_mf": (O.MODEL_CVAR, 0.002, 0.008, 0.3, 1.0, 0.4, 0),
-    "safer2": (O.MODEL_SAFER2, 0.004, 0.004, 0.3, 0.15, 0.1, 0),
-    "safer2_epan": (O.MODEL_SAFER2, 0.004, 0.004, 0.3, 0.7, 0.1, 1),
+    # model: (oracle id, reg, w, alpha, bandwidth, stepsize, epan, use_snr)
+    "ials": (O.MODEL_IALS, 0.003, 0.1, 0.3, 1.0, 0.1, 0, 0),
+    "erm_mf": (O.MODEL_ERM, 0.005, 0.004, 0.3, 1.0, 0.1, 0, 0),
+    "cvar_mf": (O.MODEL_CVAR, 0.002, 0.008, 0.3, 1.0, 0.4, 0, 0),
+    "safer2": (O.MODEL_SAFER2, 0.004, 0.004, 0.3, 0.15, 0.1, 0, 0),
+    "safer2_epan": (O.MODEL_SAFER2, 0.004, 0.004, 0.3, 0.7, 0.1, 1, 0),
+    # safer2_test.cc:37-58: sub-sampled Newton (sampling 0.5) on the seeded
+    # sample stream shared by the product (safer2.h) and the oracle
+    "safer2_snr": (O.MODEL_SAFER2, 0.004, 0.004, 0.3, 0.15, 0.1, 0, 1),
 }
+
+REPORT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out",
+                      "parity_report.jsonl")
+
+
+def report(**kw):
+    """Append one parity measurement (max / percentile row errors) to
+    gpurun_out/parity_report.jsonl -- the numbers behind the bars below."""
+    import json
+    try:
+        os.makedirs(os.path.dirname(REPORT), exist_ok=True)
+        with open(REPORT, "a") as f:
+            f.write(json.dumps(kw) + "\n")
+    except OSError:
+        pass
 
 
 @pytest.fixture(scope="module")
@@ -65,8 +83,8 @@ def ml1m_csr(ml1m):
 @pytest.mark.parametrize("case", sorted(CASES))
 @pytest.mark.parametrize("dim", [8, 32, 64, 128])
 def test_train_trajectory_matches_oracle(tmp_path, ml1m_csr, case, dim):
-    model = case.split("_epan")[0]
-    oid, reg, w, alpha, bw, eta, epan = CASES[case]
+    model = case.split("_epan")[0].split("_snr")[0]
+    oid, reg, w, alpha, bw, eta, epan, snr = CASES[case]
     # CVaR-MF's dual weights are a hard threshold (loss - xi >= 0,
     # cvar_mf.h:623) at the exact quantile of the losses, so from epoch 2 on
     # users within fp32 summation noise of xi can flip 0 <-> 1 and move whole
@@ -76,12 +94,13 @@ def test_train_trajectory_matches_oracle(tmp_path, ml1m_csr, case, dim):
     epochs = 1 if oid == O.MODEL_CVAR else 3
     out = tmp_path / "dump.bin"
     subprocess.run([os.path.join(BIN, "model_dump"), model, str(dim), str(epochs), "1", TRAIN,
-                    str(out), str(reg), str(w), str(alpha), str(bw), str(eta), str(epan)],
+                    str(out), str(reg), str(w), str(alpha), str(bw), str(eta), str(epan),
+                    str(snr), "0.5"],
                    check=True, capture_output=True, timeout=300)
     U, V, loss, dw, xi, mw, _ = _read_dump(str(out), epochs, False)
     nu, ni, up, uc, ip, ic = ml1m_csr
     m = O.Model(oid, dim, nu, ni, reg=reg, w=w, alpha=alpha, bandwidth=bw, stepsize=eta,
-                epan=bool(epan), seed=1)
+                epan=bool(epan), seed=1, use_snr=bool(snr), sampling_ratio=0.5)
     m.set_data(up, uc, ip, ic)
     m.initialize()
     for _ in range(epochs):
@@ -90,6 +109,10 @@ def test_train_trajectory_matches_oracle(tmp_path, ml1m_csr, case, dim):
     lo, wo, xo = m.state()
     # per-row relative error after `epochs` full epochs from the same seed
     eu, ev = rel_rows(U, Uo), rel_rows(V, Vo)
+    report(test="train_trajectory", case=case, dim=dim, epochs=epochs,
+           u_max=float(eu.max()), u_p999=float(np.percentile(eu, 99.9)),
+           v_max=float(ev.max()), v_p999=float(np.percentile(ev, 99.9)),
+           u_over_1e4=int((eu > 1e-4).sum()), v_over_1e4=int((ev > 1e-4).sum()))
     assert np.percentile(ev, 99.9) < 1e-4 and ev.max() < 1e-3, (ev.max(), np.percentile(ev, 99.9))
     assert np.percentile(eu, 99.9) < 1e-4 and eu.max() < 1e-3, (eu.max(), np.percentile(eu, 99.9))
     if oid != O.MODEL_IALS:
@@ -139,6 +162,17 @@ def test_gate_safer2_run_model(epan, bw):  # safer2_test.cc:17-32, 66-99, 135, 2
                       "--l2_reg", "0.004", "--bandwidth", str(bw), "--use_epanechnikov",
                       str(epan), "--xi_iterations", "5", "--pd_iterations", "1",
                       "--epoch", "10", "--print_var_stats", "1"])
+    assert _ndcg20(log) >= 0.2
+    means = [float(x) for x in re.findall(r"Min: [0-9.]+, Mean: ([0-9.]+), Max", log)]
+    assert len(means) == 10
+    assert all(abs(m - 0.3) <= 0.02 for m in means), means
+
+
+def test_gate_safer2_snr_run_model():  # safer2_test.cc:37-58, 149-185 (EXPECT_NEAR :183)
+    log = _run_model(["--model_name", "safer2", "--dim", "8", "--uobs_weight", "0.004",
+                      "--l2_reg", "0.004", "--bandwidth", "0.15", "--use_epanechnikov", "0",
+                      "--xi_iterations", "5", "--pd_iterations", "1", "--use_snr", "1",
+                      "--sampling_ratio", "0.5", "--epoch", "10", "--print_var_stats", "1"])
     assert _ndcg20(log) >= 0.2
     means = [float(x) for x in re.findall(r"Min: [0-9.]+, Mean: ([0-9.]+), Max", log)]
     assert len(means) == 10

@@ -5,7 +5,8 @@
    reference's epochs/hyper-parameters (ials_test.cc:17-45,
    erm_mf_test.cc:17-45, cvar_mf_test.cc:17-46, safer2_test.cc:17-99) and the
    SAFER2 mean dual weight within alpha +- 0.02 after every epoch
-   (safer2_test.cc:135, 183, 230; the SNR variant is not restated);
+   (safer2_test.cc:135, 183, 230), the SNR variant (safer2_test.cc:37-58,
+   sub-sampled Newton on the seeded sample stream) included;
 2. against an independent float64 numpy restatement (tests/numpy_ref.py);
 3. against libstdc++'s own std::mt19937 / std::normal_distribution<float>
    (a tiny C++ program compiled with g++ at test time).
@@ -175,7 +176,7 @@ def _run_gate(ml1m, model, epochs, dim=8, **kw):
     weights = []
     for _ in range(epochs):
         assert m.train() == 0
-        weights.append(float(m.state()[1].mean()))
+        weights.append(O.mean(m.state()[1]))  # GetMeanWeight: Eigen float mean
     Ue, rc = m.fold_in(ep, ec)
     assert rc == 0
     _, V = m.embeddings()
@@ -205,3 +206,77 @@ def test_gate_safer2(ml1m, epan, bw):  # safer2_test.cc:17-32, 66-99, 135, 230
     assert ndcg[2] >= 0.2
     for mw in weights:
         assert abs(mw - 0.3) <= 0.02
+
+
+def test_gate_safer2_snr(ml1m):  # safer2_test.cc:37-58, 149-185 (EXPECT_NEAR at :183)
+    ndcg, weights = _run_gate(ml1m, O.MODEL_SAFER2, 10, reg=0.004, w=0.004, bandwidth=0.15,
+                              xi_iterations=5, pd_iterations=1, use_snr=True, sampling_ratio=0.5)
+    assert ndcg[2] >= 0.2
+    for mw in weights:
+        assert abs(mw - 0.3) <= 0.02
+
+
+_LIBSTDCXX_PROG = r'''
+#include <cstdio>
+#include <random>
+#include <vector>
+int main() {
+  // uniform_int_distribution<int>(0, n - 1) over mt19937, as ComputeXi's
+  // SNR sampling (safer2.h:727-734) and the product's safer2.h use it
+  std::mt19937 g(777u);
+  for (int n : {1, 2, 3, 7, 1000, 4034, 116677, 2000000, 2147483647}) {
+    std::uniform_int_distribution<int> uni(0, n - 1);
+    for (int k = 0; k < 50; ++k) printf("%d\n", uni(g));
+  }
+}
+'''
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ missing")
+def test_uniform_int_matches_libstdcxx(tmp_path):
+    src = tmp_path / "uni.cc"
+    src.write_text(_LIBSTDCXX_PROG)
+    exe = tmp_path / "uni"
+    subprocess.run(["g++", "-O2", "-o", str(exe), str(src)], check=True)
+    ref = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                          check=True).stdout.split()]
+    import ctypes
+    g = (ctypes.c_uint32 * 626)()
+    O.lib().oracle_mt_seed(g, 777)
+    got = []
+    for n in (1, 2, 3, 7, 1000, 4034, 116677, 2000000, 2147483647):
+        got += [int(O.lib().oracle_uniform_int(g, n)) for _ in range(50)]
+    assert got == ref
+
+
+@pytest.mark.parametrize("n", [1, 5, 15, 16, 17, 31, 32, 33, 47, 48, 64, 100, 4034, 116677])
+def test_eigen_mean_restatement(n):
+    """The packet-sum restatement is a float sum: equal to the exact mean to
+    fp32 summation accuracy, and identical between oracle and a direct
+    Python transcription of the same order."""
+    x = np.random.default_rng(n).random(n).astype(np.float32)
+    m = O.mean(x)
+    assert abs(m - float(x.astype(np.float64).mean())) <= 1e-6 * max(1, n ** 0.5)
+    P = 16
+    f = np.float32
+    al, al2 = n // P * P, n // (2 * P) * (2 * P)
+    if al == 0:
+        r = x[0]
+        for v in x[1:]:
+            r = f(r + v)
+    else:
+        p0 = x[:P].copy()
+        if al > P:
+            p1 = x[P:2 * P].copy()
+            for i in range(2 * P, al2, 2 * P):
+                p0 = (p0 + x[i:i + P]).astype(f)
+                p1 = (p1 + x[i + P:i + 2 * P]).astype(f)
+            p0 = (p0 + p1).astype(f)
+            if al > al2:
+                p0 = (p0 + x[al2:al2 + P]).astype(f)
+        s8 = (p0[:8] + p0[8:]).astype(f)
+        s4 = (s8[:4] + s8[4:]).astype(f)
+        r = f(f(s4[0] + s4[2]) + f(s4[1] + s4[3]))
+        for v in x[al:]:
+            r = f(r + v)
+    assert np.float32(m) == np.float32(r / f(n))

@@ -209,14 +209,56 @@ def test_eval_side_fold_in(ml1m):
     assert rel_rows(Ue, Uo).max() < TOL_ROW
 
 
-def test_not_spd_reported(quirk_data):
+@pytest.mark.parametrize("dim", [64, 128, 256])
+def test_not_spd_reported(quirk_data, dim):
+    # d = 64 runs the 4-wave Cholesky, d >= 96 the 8-wave dataflow one whose
+    # forward substitution has its own wave (chol.h chol_solve_df, NW >= 8)
     nu, ni, up, uc, ip, ic = quirk_data
-    ctx, U, V = _ctx(64, nu, ni, up, uc, ip, ic)
+    ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
     ctx.gramian(fh.SIDE_ITEM)
     with pytest.raises(fh.FrecsysError) as ei:
         ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, -50.0, 0.1)  # negative lambda
     assert ei.value.code == fh.ERR_NOT_SPD
     assert 0 <= ei.value.entity < nu
+
+
+def _rank_deficient_case(dim):
+    """40 items at d = 64..256: G = V^T V has rank <= 40, so with a vanishing
+    lambda both M = w G + lam I (history space) and A (d space) are singular
+    up to fp32 rounding -- pivots fail on either path."""
+    rng = np.random.default_rng(11)
+    nu, ni = 100, 40
+    users = np.repeat(np.arange(nu), 12)
+    items = np.concatenate([rng.choice(ni, 12, replace=False) for _ in range(nu)])
+    from frecsys_hip.data import _csr_from_pairs
+    up, uc = _csr_from_pairs(users, items, nu)
+    ip, ic = _csr_from_pairs(items, users, ni)
+    return nu, ni, up, uc, ip, ic
+
+
+@pytest.mark.parametrize("dim", [64, 128, 256])
+def test_not_spd_history_space_falls_back(monkeypatch, dim):
+    """A failed history-space pivot reruns the whole call on the d-space
+    path, so the verdict (error code, entity, or the rows) is exactly the
+    FRECSYS_DUAL=0 one."""
+    nu, ni, up, uc, ip, ic = _rank_deficient_case(dim)
+    res = []
+    for dual in ("0", "1"):
+        monkeypatch.setenv("FRECSYS_DUAL", dual)
+        ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+        ctx.gramian(fh.SIDE_ITEM)
+        try:
+            ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, 1e-35, 1.0)
+            res.append((0, -1, ctx.get_embeddings(fh.SIDE_USER)))
+        except fh.FrecsysError as e:
+            res.append((e.code, e.entity, None))
+        res[-1] += (ctx.timing("solve_user")[1], ctx.timing("solve_user.hspace")[1])
+        ctx.close()
+    (c0, e0, x0, n0, _), (c1, e1, x1, n1, hs1) = res
+    assert hs1 == 1 and n1 == 2 and n0 == 1  # history space ran, failed, d-space reran
+    assert (c1, e1) == (c0, e0)
+    if c0 == 0:
+        np.testing.assert_array_equal(x1, x0)
 
 
 def test_bad_csr_rejected(quirk_data):
