@@ -1,6 +1,7 @@
 # Build of the MI355X (gfx950) solve loop.  Driven by __graft_entry__.build()
 # (`make -j8 all`); everything lands in-tree so it travels to the GPU box.
 #   libfrecsys_hip.so  -- HIP kernels + C-ABI (include/frecsys_hip.h)
+#   libfrecsys_model.so -- C-ABI of the model classes (include/frecsys_model.h)
 #   run_model          -- reference-compatible CLI (C++ host over the C-ABI)
 #   liboracle.so       -- CPU restatement, TEST INFRASTRUCTURE ONLY
 PKG      := safer2-recommender_amd
@@ -10,6 +11,7 @@ LIB      := $(PKG)/frecsys_hip/libfrecsys_hip.so
 ORACLE   := oracle/liboracle.so
 RUNMODEL := $(PKG)/bin/run_model
 MODELDUMP := $(PKG)/bin/model_dump
+MODELLIB := $(PKG)/frecsys_hip/libfrecsys_model.so
 ARCH     ?= gfx950
 HIPCC    ?= /opt/rocm/bin/hipcc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
@@ -21,8 +23,9 @@ HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/dual.hip $(CSRC)/spectral.hip $(CSRC)/gram
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
 HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h $(CSRC)/chol.h include/frecsys_hip.h
 
-.PHONY: all lib oracle run_model model_dump clean ablation
-all: lib oracle run_model model_dump
+.PHONY: all lib oracle run_model model_dump model_lib clean ablation
+all: lib oracle run_model model_dump model_lib
+model_lib: $(MODELLIB)
 lib: $(LIB)
 oracle: $(ORACLE)
 run_model: $(RUNMODEL)
@@ -44,8 +47,12 @@ $(RUNMODEL): $(PKG)/tools/run_model.cc $(FRECSYS_HDRS) include/frecsys_hip.h $(L
 	g++ $(CXXFLAGS) -o $@ $(PKG)/tools/run_model.cc -L$(PKG)/frecsys_hip -lfrecsys_hip \
 	    -Wl,-rpath,'$$ORIGIN/../frecsys_hip'
 
+$(MODELLIB): $(PKG)/tools/model_capi.cc $(FRECSYS_HDRS) include/frecsys_hip.h include/frecsys_model.h $(LIB)
+	g++ $(CXXFLAGS) -fPIC -shared -o $@ $(PKG)/tools/model_capi.cc -L$(PKG)/frecsys_hip -lfrecsys_hip \
+	    -Wl,-rpath,'$$ORIGIN'
+
 clean:
-	rm -rf $(OBJ) $(LIB) $(ORACLE) $(PKG)/bin
+	rm -rf $(OBJ) $(LIB) $(MODELLIB) $(ORACLE) $(PKG)/bin
 
 $(MODELDUMP): tests/cpp/model_dump.cc $(FRECSYS_HDRS) include/frecsys_hip.h $(LIB)
 	@mkdir -p $(PKG)/bin

@@ -1,38 +1,48 @@
 #!/usr/bin/env python3
-"""bench.py -- iALS closed-form solve loop on MI355X (BASELINE.json configs[1]).
+"""bench.py -- the closed-form solve loop on MI355X, timed through the product's
+own Train() (include/frecsys_model.h -> the C++ model classes -> libfrecsys_hip.so).
 
-Workload (N=1 and every N): iALS, dim 256, ML-20M-shaped synthetic data
-(116,677 users x 20,108 items, ~8.54M interactions, seed 98765; README.md:84
-hyperparameters w=0.1, l2_reg=0.003), embeddings N(0, 0.1/sqrt(d)) seed 1.
-A "step" is one full Train() epoch (ials.h:187-206 with print_train_stats
-off): U half-step (G_V, solve all users, all-gather U), V half-step (G_U,
-solve all items, all-gather V), G_V + ComputeUserLoss.  Inputs are resident
-in HBM before the timed region.  With N GPUs (torchrun, one process per GPU)
-users and items are split nnz-balanced across ranks, Gramian partials are
-all-reduced and factor shards all-gathered over RCCL: the total work is
-fixed, so scaling is "strong".
+Headline (the JSON line's top level; BASELINE.json configs[1]): iALS, dim 256,
+ML-20M-shaped synthetic data (116,677 users x 20,108 items, ~8.54M interactions,
+seed 98765), README.md:84 hyperparameters (w=0.1, l2_reg=0.003, reg_exp 1),
+stdev 0.1, init seed 1, print_train_stats 0.  A "step" is one
+`IALSRecommender::Train()` call (ials.h:187-206): U half-step (Gramian of V,
+solve all users, all-gather U), V half-step, Gramian + ComputeUserLoss.  Inputs
+are resident in HBM before the timed region.  With N GPUs (torchrun, one process
+per GPU) users and items are split nnz-balanced across ranks, Gramian partials
+all-reduced and factor shards all-gathered over RCCL: the total work is fixed
+("strong" scaling).
 
 value = users updated per second of training wall time = N_users * K / T,
 T = max over ranks of the K-epoch wall time.  sec_per_epoch = T / K.
 
-roofline: the dominant kernel is solve_tiled_kernel<8, false, true>, the
-d x d solve of the long histories (h > 256; the shorter ones take the
-history-space path): gather + MFMA assembly (its fp32
-products on the bf16 matrix cores as 3-piece splits, fp32-accurate) +
-dataflow blocked Cholesky, compute-bound, priced against the fp32 MFMA
-peak (157.3 TFLOP/s) since the algorithm is fp32.
-Algorithmic flops per launch = sum over its entities of h*d*(d+1) (0 for
-the histories > 2048 rows whose SYRK the split kernel did) + d^3/3 + 2*d^2
-(SURVEY 8(d)); duration = its HIP-event time (both half-steps averaged).
-`paths` reports the same figures for the other kernels of the epoch.
+`workloads` carries the same measurement for BASELINE configs[2] (SAFER2 d=256
+ML-20M-shaped, README.md:79 flags, pd=1 xi=5 use_snr=1 sampling_ratio=0.1) and
+configs[3] (iALS d=512 MSD-shaped, README.md:105), each with its own roofline,
+gather roofline and cpu_baseline; `--workload` runs one of them (or config 5,
+SAFER2 d=1024 2M x 500K, which is opt-in: its data alone takes minutes).
 
-cpu_baseline: the CPU restatement (oracle/, "port") timing the same U
-half-step on a bounded contiguous sample of users, threads = the box's CPU
-share (OMP_NUM_THREADS, 16 on the GPU box).
+roofline: the dominant kernel of the workload, priced against the fp32 MFMA peak
+(157.3 TFLOP/s; the algorithm is fp32 and compute-bound): algorithmic flops per
+launch (h*d*(d+1) SYRK + d^3/3 + 2d^2 solve per d-space entity) /
+its HIP-event launch time.  gather_roofline: SURVEY 8(d)'s gather bytes of both
+half-steps (nnz*d*4 + nnz*4 + (N+1)*8 + N*d*4 per side) / the solve time of both
+half-steps, vs 8 TB/s -- the north-star figure at d=512 on the MSD shape.
+loss_gather_roofline: the same bytes of the ComputeUserLoss pass (a pure
+embedding gather) / its time.
+
+cpu_baseline: the CPU restatement (oracle/, kind "port") timing the same U
+half-step on a bounded contiguous user sample on this host's CPU share.
+
+The shipped library has no knobs that skip work; bench.py refuses to run with
+any FRECSYS_* variable set (they select paths for profiling) unless
+--allow-env is given, and then records them in the line as "frecsys_env".
 """
 import argparse
 import json
 import os
+import platform
+import subprocess
 import sys
 import time
 
@@ -44,8 +54,28 @@ sys.path.insert(0, os.path.join(ROOT, "safer2-recommender_amd"))
 import frecsys_hip as fh  # noqa: E402
 from frecsys_hip.data import SHAPES, synthetic  # noqa: E402
 
-PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix/vector peak (spec)
+PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (spec)
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+# BASELINE.json configs; flags are the run_model flags (README.md lines cited).
+WORKLOADS = {
+    "ials_ml20m_d256": dict(
+        config=1, model="ials", shape="ml20m", dim=256, readme="README.md:84",
+        flags=dict(l2_reg=0.003, uobs_weight=0.1, l2_reg_exp=1.0)),
+    "safer2_ml20m_d256": dict(
+        config=2, model="safer2", shape="ml20m", dim=256, readme="README.md:79",
+        flags=dict(l2_reg=0.002, uobs_weight=0.002, alpha=0.3, bandwidth=0.18, pd_iterations=1,
+                   xi_iterations=5, use_snr=True, sampling_ratio=0.1)),
+    "ials_msd_d512": dict(
+        config=3, model="ials", shape="msd", dim=512, readme="README.md:105",
+        flags=dict(l2_reg=0.002, uobs_weight=0.05, l2_reg_exp=1.0)),
+    "safer2_2m500k_d1024": dict(
+        config=4, model="safer2", shape="2m500k", dim=1024, readme="README.md:100",
+        flags=dict(l2_reg=0.0012, uobs_weight=0.0004, alpha=0.3, bandwidth=0.1,
+                   pd_iterations=1, xi_iterations=5, use_snr=True, sampling_ratio=0.1)),
+}
+HEADLINE = "ials_ml20m_d256"
+DEFAULT_EXTRAS = ("safer2_ml20m_d256", "ials_msd_d512")
 
 
 def parse():
@@ -53,12 +83,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--shape", default="ml20m")
-    ap.add_argument("--dim", type=int, default=256)
-    ap.add_argument("--reg", type=float, default=0.003)
-    ap.add_argument("--uobs_weight", type=float, default=0.1)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="target CPU-baseline sample duration (0 disables)")
+    ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
+    ap.add_argument("--extras", default=",".join(DEFAULT_EXTRAS),
+                    help="comma-separated extra workloads measured after the headline "
+                         "('' for none)")
+    ap.add_argument("--extra-steps", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU-baseline sample duration per workload (0 disables)")
+    ap.add_argument("--allow-env", action="store_true",
+                    help="run although FRECSYS_* variables are set (recorded in the line)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -68,40 +101,271 @@ def log(msg, rank=0):
         print(msg, file=sys.stderr, flush=True)
 
 
-def ials_epoch(ctx, args, gv_fresh):
-    """One IALSRecommender::Train (ials.h:187-206) over the C-ABI."""
-    if not gv_fresh:
-        ctx.gramian(fh.SIDE_ITEM, fetch=False)                 # ials.h:321 (V)
-    ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, args.reg, args.uobs_weight)
-    ctx.gramian(fh.SIDE_USER, fetch=False)                     # ials.h:321 (U)
-    ctx.solve_side(fh.SIDE_ITEM, fh.KIND_IALS, args.reg, args.uobs_weight)
-    ctx.gramian(fh.SIDE_ITEM, fetch=False)                     # ials.h:371
-    ctx.user_loss(fh.SIDE_USER, args.uobs_weight, False, fetch=False)
+def frecsys_env():
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("FRECSYS_")}
 
 
-def cpu_baseline(up, uc, V, args, nthreads):
-    """Oracle U half-step on a bounded contiguous user sample."""
+def host_cpu_share():
+    """Threads for the CPU baseline: this process's CPU share (affinity,
+    bounded by a cgroup quota and OMP_NUM_THREADS when set), and what the
+    host reports."""
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    info["affinity"] = aff
+    share = aff
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            info["cgroup_quota_cpus"] = float(q) / float(p)
+            share = min(share, max(1, int(float(q) / float(p))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        info["omp_num_threads"] = int(omp)
+        share = min(share, int(omp))
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                info["model"] = line.split(":", 1)[1].strip()
+            if line.startswith("Flags:"):
+                info["avx512f"] = " avx512f " in line + " "
+    except (OSError, subprocess.SubprocessError):
+        info["model"] = platform.processor()
+    return share, info
+
+
+def heff_fn(model, side, quirks=True):
+    """Rows the assembly reads per entity (h, plus the ProjectV tail-quirk
+    rows of the weighted V kinds, safer2.h:196-208)."""
+    if model in ("safer2", "erm_mf", "cvar_mf") and side == fh.SIDE_ITEM and quirks:
+        return lambda h: np.where((h > 128) & (h % 128 != 0), h + 128 - h % 128, h)
+    return lambda h: h
+
+
+def path_accounting(ctx, spec, ptrs, timers, K):
+    """Algorithmic work per solve path of both half-steps."""
+    d = spec["dim"]
+    Dp = fh.padded_dim(d)
+    wide = Dp > 256
+    dual_max, split_rows = 256, 1024
+    chol = d ** 3 / 3.0 + 2.0 * d * d
+    fin_flops, fin_ms, fin_n = 0.0, 0.0, 0
+    paths = {}
+    for side, ptr, name in ((fh.SIDE_USER, ptrs[0], "solve_user"),
+                            (fh.SIDE_ITEM, ptrs[1], "solve_item")):
+        lo_, hi_ = ctx.shard_range(side)
+        hs = np.diff(ptr)[lo_:hi_].astype(np.float64)
+        hs = hs[hs > 0]
+        he = heff_fn(spec["model"], side)(hs)
+        ds = he[he > dual_max] if Dp >= 64 else he
+        if wide or split_rows <= 0:
+            unsplit, split = ds, ds[:0]
+        else:
+            unsplit, split = ds[ds <= 2 * split_rows], ds[ds > 2 * split_rows]
+        f_fin = float(np.sum(unsplit) * d * (d + 1) + len(ds) * chol)
+        ms, n = timers[name + ".dspace"]
+        if n:
+            fin_flops += f_fin * n / max(K, 1)
+            fin_ms += ms
+            fin_n += n
+        hsp = he[he <= dual_max] if Dp >= 64 else he[:0]
+        hp = 32.0 * np.ceil(hsp / 32.0)
+        sp_ms, sp_n = timers[name + ".split"]
+        hs_ms, hs_n = timers[name + ".hspace"]
+        paths[name] = {
+            "dspace_entities": int(len(ds)), "dspace_ms": ms / max(K, 1),
+            "dspace_tflops": f_fin / (ms / max(n, 1) * 1e-3) / 1e12 if n else None,
+            "split_rows_total": float(np.sum(split)),
+            "split_ms": sp_ms / max(K, 1),
+            "split_tflops": (float(np.sum(split)) * d * (d + 1) / (sp_ms / sp_n * 1e-3) / 1e12)
+            if sp_n else None,
+            "hspace_entities": int(len(hsp)), "hspace_ms": hs_ms / max(K, 1),
+            # history-space algorithmic flops: h_p^2 * Dp (SYRK of S) + h_p^3 / 3
+            "hspace_tflops": (float(np.sum(hp * hp * Dp + hp ** 3 / 3.0))
+                              / (hs_ms / max(K, 1) * 1e-3) / 1e12) if hs_n else None,
+            "basis_ms": timers[name + ".basis"][0] / max(K, 1),
+            "rotate_ms": timers[name + ".rotate"][0] / max(K, 1),
+        }
+    avg_ms = fin_ms / max(fin_n, 1)
+    flops = fin_flops / max(fin_n / max(K, 1), 1)  # per launch
+    return paths, avg_ms, flops
+
+
+def gather_bytes(ptr, lo, hi, d, out_floats):
+    """SURVEY 8(d) gather bytes of one pass over rows [lo, hi): every history
+    row of the other side (d floats) + its int32 id + row_ptr + the output."""
+    nnz = float(ptr[hi] - ptr[lo])
+    n = hi - lo
+    return nnz * d * 4 + nnz * 4 + (n + 1) * 8 + n * out_floats * 4
+
+
+def load_pmc(workload):
+    path = os.path.join(ROOT, "profiles", "latest_pmc.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        js = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    w = js.get("workloads", {}).get(workload)
+    if not w:
+        return None, None
+    return w.get("dominant_traffic_bytes"), js.get("source")
+
+
+def cpu_baseline(spec, up, uc, V, seconds, nthreads, host):
+    """Oracle U half-step (kind of the workload's U step, Gramian excluded) on
+    a bounded contiguous user sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
+    f = spec["flags"]
     G = O.gramian(V, nthreads=nthreads)
     n = len(up) - 1
-    # calibrate on a small sample, then size the sample to ~cpu_seconds
-    k = min(n, 256)
-    t0 = time.perf_counter()
-    O.step(up[:k + 1], uc[:up[k]], V, G, 0, args.reg, args.uobs_weight, nthreads=nthreads)
-    dt = time.perf_counter() - t0
-    k2 = int(min(n, max(k, k * args.cpu_seconds / max(dt, 1e-6))))
-    t0 = time.perf_counter()
-    _, rc = O.step(up[:k2 + 1], uc[:up[k2]], V, G, 0, args.reg, args.uobs_weight,
-                   nthreads=nthreads)
-    dt = time.perf_counter() - t0
+    if spec["model"] == "ials":
+        kind, reg, w, extra = 0, f["l2_reg"], f["uobs_weight"], {}
+    else:  # ProjectU with omega = alpha (the first SAFER2 epoch's weights)
+        kind, reg, w = 1, f["l2_reg"], f["uobs_weight"]
+        extra = {"entity_weight": np.full(n, f["alpha"], np.float32)}
+
+    def run(k):
+        ex = {kk: vv[:k] for kk, vv in extra.items()}
+        t0 = time.perf_counter()
+        O.step(up[:k + 1], uc[:up[k]], V, G, kind, reg, w, nthreads=nthreads, **ex)
+        return time.perf_counter() - t0
+
+    k = min(n, 64)
+    dt = run(k)
+    k2 = int(min(n, max(k, k * seconds / max(dt, 1e-6))))
+    dt = run(k2)
     return {"value": k2 / dt, "unit": "user-solve updates/s", "cores": nthreads, "kind": "port",
-            "sample": f"oracle iALS U half-step (Gramian excluded) on users 0..{k2 - 1} of the "
-                      f"same synthetic ML-20M-shaped data, d={args.dim}, {dt:.1f} s"}
+            "host": host,
+            "sample": f"oracle {spec['model']} U half-step (kind {kind}, Gramian excluded) on "
+                      f"users 0..{k2 - 1} of the same synthetic {spec['shape']}-shaped data, "
+                      f"d={spec['dim']}, {dt:.1f} s on {nthreads} threads; a faithful fp32 C "
+                      f"restatement (naive SYRK + unblocked LLT), not Eigen itself"}
+
+
+def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, warmup, cpu_s):
+    spec = WORKLOADS[name]
+    t0 = time.time()
+    if spec["shape"] not in data_cache:
+        data_cache.clear()  # one shape resident at a time
+        data_cache[spec["shape"]] = synthetic(SHAPES[spec["shape"]])
+    up, uc, ip, ic = data_cache[spec["shape"]]
+    nu, ni = len(up) - 1, len(ip) - 1
+    nnz = int(up[-1])
+    log(f"[bench] {name}: data {nu} users x {ni} items, nnz {nnz} ({time.time() - t0:.1f}s)", rank)
+    users = np.repeat(np.arange(nu, dtype=np.int32), np.diff(up))
+    cid = None
+    if world > 1:
+        obj = [fh.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        cid = obj[0]
+    model = fh.Model(spec["model"], users, uc, dim=spec["dim"], stdev=0.1, seed=1,
+                     print_train_stats=False, device=local_rank, world=world, rank=rank,
+                     comm_id=cid, **spec["flags"])
+    del users
+    ctx = model.context()
+    model.initialize()  # run_model.cc:246-257 (SAFER2); outside the timed region
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    model.train(warmup)
+    ctx.timing_reset()
+    barrier()
+    t_start = time.perf_counter()
+    for s in range(steps):
+        model.train(1)
+        if not args.quiet:
+            log(f"[bench] {name} step {s + 1}/{steps} done", rank)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    K = steps
+    d = spec["dim"]
+    Dp = fh.padded_dim(d)
+    names = ["solve_user", "solve_item", "gramian", "user_loss", "allgather", "allreduce"]
+    names += [f"{s}.{p}" for s in ("solve_user", "solve_item")
+              for p in ("dspace", "split", "basis", "hspace", "rotate")]
+    timers = {k: ctx.timing(k) for k in names}
+    paths, avg_ms, flops = path_accounting(ctx, spec, (up, ip), timers, K)
+    achieved_tf = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+    ulo, uhi = ctx.shard_range(fh.SIDE_USER)
+    ilo, ihi = ctx.shard_range(fh.SIDE_ITEM)
+    su_ms = timers["solve_user"][0] / max(K, 1)
+    si_ms = timers["solve_item"][0] / max(K, 1)
+    gb = gather_bytes(up, ulo, uhi, d, d) + gather_bytes(ip, ilo, ihi, d, d)
+    g_gbs = gb / ((su_ms + si_ms) * 1e-3) / 1e9 if su_ms + si_ms > 0 else 0.0
+    loss_ms = timers["user_loss"][0] / max(timers["user_loss"][1], 1)
+    lb = gather_bytes(up, ulo, uhi, d, 1)
+    l_gbs = lb / (loss_ms * 1e-3) / 1e9 if loss_ms > 0 else 0.0
+    traffic, traffic_src = load_pmc(name) if world == 1 else (None, None)
+    wide = Dp > 256
+    res = {
+        "workload": name,
+        "baseline_config": f"BASELINE.json configs[{spec['config']}]",
+        "model": spec["model"], "flags": spec["flags"], "flags_source": spec["readme"],
+        "n_users": nu, "n_items": ni, "nnz": nnz, "dim": d, "padded_dim": Dp,
+        "value": nu * K / elapsed, "unit": "user-solve updates/s",
+        "steps": K, "warmup": warmup,
+        "ms_per_step": elapsed / K * 1e3, "sec_per_epoch": elapsed / K,
+        "u_halfstep_solve_updates_per_s": ((uhi - ulo) / (su_ms * 1e-3)) * world if su_ms else None,
+        "kernel_ms_per_epoch": {k: v[0] / max(K, 1) for k, v in timers.items()},
+        "roofline": {"bound": "mfma",
+                     "kernel": ("wide_syrk_kernel + wide_chol_kernel (batched d-space solve, "
+                                "A in an HBM workspace)") if wide else
+                               ("solve_tiled_kernel<8, false, true> (d-space solve: split-bf16 "
+                                "MFMA SYRK + fp32 dataflow Cholesky)"),
+                     "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "avg_launch_ms": avg_ms, "flops_per_launch": flops},
+        "paths": paths,
+        "gather_roofline": {"bound": "hbm", "scope": "both half-steps' solves (SURVEY 8(d) "
+                                                     "gather bytes / solve time)",
+                            "achieved": g_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": g_gbs / PEAK_HBM_GBS, "bytes_per_step": gb},
+        "loss_gather_roofline": {"bound": "hbm", "scope": "ComputeUserLoss pass (loss_gather + "
+                                                          "quad kernels)",
+                                 "achieved": l_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                 "frac": l_gbs / PEAK_HBM_GBS, "bytes_per_launch": lb},
+    }
+    if spec["model"] != "ials":
+        res["mean_dual_weight"] = model.mean_weight()
+    if cpu_s > 0 and world == 1 and rank == 0:
+        try:
+            nthreads, host = host_cpu_share()
+            V = ctx.get_embeddings(fh.SIDE_ITEM)
+            res["cpu_baseline"] = cpu_baseline(spec, up, uc, V, cpu_s, nthreads, host)
+        except Exception as e:  # the baseline must never kill the bench line
+            log(f"[bench] cpu baseline failed: {e}")
+            res["cpu_baseline"] = None
+    else:
+        res["cpu_baseline"] = None
+    ctx.close()
+    model.close()
+    return res
 
 
 def main():
     args = parse()
+    env = frecsys_env()
+    if env and not args.allow_env:
+        sys.exit(f"bench.py: refusing to run with {sorted(env)} set (profiling path selectors; "
+                 f"pass --allow-env to run anyway, recorded in the line)")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -113,157 +377,46 @@ def main():
         tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         dist = tdist
 
-    shape = SHAPES[args.shape]
-    t0 = time.time()
-    up, uc, ip, ic = synthetic(shape)
-    nu, ni = len(up) - 1, len(ip) - 1
-    nnz = int(up[-1])
-    log(f"[bench] data {args.shape}: {nu} users x {ni} items, nnz {nnz} "
-        f"({time.time() - t0:.1f}s)", rank)
-
-    ctx = fh.Context(args.dim, nu, ni, device=local_rank)
-    if world > 1:
-        import torch
-        obj = [fh.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        ctx.comm_init(world, rank, obj[0])
-    ctx.load_csr(fh.SIDE_USER, up, uc)
-    ctx.load_csr(fh.SIDE_ITEM, ip, ic)
-    ctx.init_embeddings(1, 0.1)
-
-    def barrier():
-        ctx.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    ctx.gramian(fh.SIDE_ITEM, fetch=False)
-    gv_fresh = True
-    for _ in range(args.warmup):
-        ials_epoch(ctx, args, gv_fresh)
-    ctx.timing_reset()
-    barrier()
-    t_start = time.perf_counter()
-    for s in range(args.steps):
-        ials_epoch(ctx, args, gv_fresh)
-        if not args.quiet:
-            log(f"[bench] step {s + 1}/{args.steps} done", rank)
-    barrier()
-    elapsed = time.perf_counter() - t_start
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    K = args.steps
-    d = args.dim
-    Dp = fh.padded_dim(d)
-    names = ["solve_user", "solve_item", "gramian", "user_loss", "allgather", "allreduce"]
-    names += [f"{s}.{p}" for s in ("solve_user", "solve_item")
-              for p in ("dspace", "split", "basis", "hspace", "rotate")]
-    timers = {k: ctx.timing(k) for k in names}
-
-    # d-space entities of this rank (iALS: h_eff = h), split ones (> 2 * 1024)
-    dual_max = int(os.environ.get("FRECSYS_DUAL_MAX_H", "256"))
-    split_rows = int(os.environ.get("FRECSYS_SPLIT_ROWS", "1024"))
-    dual_on = os.environ.get("FRECSYS_DUAL", "1") != "0" and Dp >= 64
-    chol = d ** 3 / 3.0 + 2.0 * d * d
-    fin_flops, fin_ms, fin_n = 0.0, 0.0, 0
-    paths = {}
-    for side, ptr, name in ((fh.SIDE_USER, up, "solve_user"), (fh.SIDE_ITEM, ip, "solve_item")):
-        lo_, hi_ = ctx.shard_range(side)
-        hs = np.diff(ptr)[lo_:hi_].astype(np.float64)
-        hs = hs[hs > 0]
-        ds = hs[hs > dual_max] if dual_on else hs
-        unsplit = ds[ds <= 2 * split_rows] if split_rows > 0 else ds
-        split = ds[ds > 2 * split_rows] if split_rows > 0 else ds[:0]
-        f_fin = float(np.sum(unsplit) * d * (d + 1) + len(ds) * chol)
-        ms, n = timers[name + ".dspace"]
-        if n:
-            fin_flops += f_fin * n / max(K, 1)
-            fin_ms += ms
-            fin_n += n
-        hsp = hs[hs <= dual_max] if dual_on else hs[:0]
-        hp = 32.0 * np.ceil(hsp / 32.0)
-        paths[name] = {
-            "dspace_entities": int(len(ds)), "dspace_ms": ms / max(K, 1),
-            "dspace_tflops": f_fin / (ms / max(n, 1) * 1e-3) / 1e12 if n else None,
-            "split_rows_total": float(np.sum(split)),
-            "split_ms": timers[name + ".split"][0] / max(K, 1),
-            "split_tflops": (float(np.sum(split)) * d * (d + 1)
-                             / (timers[name + ".split"][0] / max(timers[name + ".split"][1], 1)
-                                * 1e-3) / 1e12) if timers[name + ".split"][1] else None,
-            "hspace_entities": int(len(hsp)), "hspace_ms": timers[name + ".hspace"][0] / max(K, 1),
-            # history-space algorithmic flops: h_p^2 * Dp (SYRK of S) + h_p^3 / 3
-            "hspace_tflops": (float(np.sum(hp * hp * Dp + hp ** 3 / 3.0))
-                              / (timers[name + ".hspace"][0] / max(K, 1) * 1e-3) / 1e12)
-            if timers[name + ".hspace"][1] else None,
-            "basis_ms": timers[name + ".basis"][0] / max(K, 1),
-            "rotate_ms": timers[name + ".rotate"][0] / max(K, 1),
-        }
-    avg_ms = fin_ms / max(fin_n, 1)
-    flops = fin_flops / max(fin_n / max(K, 1), 1)  # per launch
-    achieved_tf = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
-    n_own = ctx.shard_range(fh.SIDE_USER)[1] - ctx.shard_range(fh.SIDE_USER)[0]
-    su_ms = timers["solve_user"][0] / max(K, 1)
-    h_all = np.diff(up).astype(np.float64)
-    gather_bytes = float(h_all.sum() * d * 4 + h_all.sum() * 4 + (n_own + 1) * 8 + n_own * d * 4)
-    gather_gbs = gather_bytes / (su_ms * 1e-3) / 1e9 if su_ms > 0 else 0.0
-
-    traffic = None
-    traffic_src = None
-    pmc = os.path.join(ROOT, "profiles", "latest_pmc.json")
-    if os.path.exists(pmc) and world == 1:
-        try:
-            js = json.load(open(pmc))
-            traffic = js.get("dspace_traffic_bytes")
-            traffic_src = js.get("source")
-        except Exception:
-            traffic = None
+    data_cache = {}
+    head = run_workload(args.workload, args, world, rank, local_rank, dist, data_cache,
+                        args.steps, args.warmup, args.cpu_seconds)
+    extras = []
+    for name in [x for x in args.extras.split(",") if x and x != args.workload]:
+        extras.append(run_workload(name, args, world, rank, local_rank, dist, data_cache,
+                                   args.extra_steps, 1, args.cpu_seconds))
     if rank == 0:
-        cpu = None
-        if args.cpu_seconds > 0 and world == 1:
-            nthreads = min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), os.cpu_count() or 1)
-            V = ctx.get_embeddings(fh.SIDE_ITEM)
-            try:
-                cpu = cpu_baseline(up, uc, V, args, nthreads)
-            except Exception as e:  # the baseline must never kill the bench line
-                log(f"[bench] cpu baseline failed: {e}")
+        spec = WORKLOADS[args.workload]
         line = {
-            "metric": "user-solve updates/sec + sec/epoch, iALS dim=256 ML-20M shape",
-            "value": nu * K / elapsed,
+            "metric": "user-solve updates/sec + sec/epoch, "
+                      f"{spec['model'].upper() if spec['model'] == 'safer2' else 'iALS'} "
+                      f"dim={spec['dim']} {spec['shape']}-shaped",
+            "value": head["value"],
             "unit": "user-solve updates/s",
             "n_gpus": world,
-            "steps": K,
+            "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / K * 1e3,
-            "sec_per_epoch": elapsed / K,
+            "ms_per_step": head["ms_per_step"],
+            "sec_per_epoch": head["sec_per_epoch"],
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (ML-20M-shaped, Zipf-Mandelbrot items, lognormal users, seed 98765)",
-            "config": {"workload": f"iALS d={d} {args.shape}-shaped synthetic, full Train() epoch",
-                       "n_users": nu, "n_items": ni, "nnz": nnz, "dim": d, "padded_dim": Dp,
-                       "l2_reg": args.reg, "uobs_weight": args.uobs_weight,
-                       "parallelism": f"entity-sharded x{world}"},
-            "u_halfstep_solve_updates_per_s": (n_own / (su_ms * 1e-3)) * world if su_ms else None,
-            "kernel_ms_per_epoch": {k: v[0] / max(K, 1) for k, v in timers.items()},
-            "roofline": {"bound": "mfma",
-                         "kernel": "solve_tiled_kernel<8, false, true> (d-space solve: split-bf16 "
-                                   "MFMA SYRK + fp32 dataflow Cholesky)",
-                         "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "avg_launch_ms": avg_ms, "flops_per_launch": flops},
-            "paths": paths,
-            "gather_roofline": {"bound": "hbm", "scope": "whole user half-step",
-                                "achieved": gather_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                "frac": gather_gbs / PEAK_HBM_GBS, "bytes_per_step": gather_bytes},
-            "cpu_baseline": cpu,
+            "data": f"synthetic ({spec['shape']}-shaped, Zipf-Mandelbrot items, lognormal users, "
+                    "seed 98765); random init seed 1",
+            "config": {"workload": f"{head['workload']}: {spec['model']} d={spec['dim']} "
+                                   f"{spec['shape']}-shaped synthetic, one Train() epoch per step "
+                                   f"({spec['readme']} flags, print_train_stats 0)",
+                       "n_users": head["n_users"], "n_items": head["n_items"],
+                       "nnz": head["nnz"], "dim": head["dim"], "padded_dim": head["padded_dim"],
+                       "flags": spec["flags"], "parallelism": f"entity-sharded x{world}"},
+            "timed_path": "frecsys_model_train -> Recommender::Train (include/frecsys_model.h)",
+            "frecsys_env": env,
         }
+        for k in ("u_halfstep_solve_updates_per_s", "kernel_ms_per_epoch", "roofline", "paths",
+                  "gather_roofline", "loss_gather_roofline", "cpu_baseline"):
+            line[k] = head[k]
+        line["workloads"] = {r["workload"]: r for r in extras}
         print(json.dumps(line), flush=True)
-    ctx.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -24,6 +24,7 @@ OK = 0
 ERR_INVALID, ERR_HIP, ERR_RCCL, ERR_NOT_SPD, ERR_NAN, ERR_UNSUPPORTED, ERR_NO_DEVICE = range(1, 8)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfrecsys_hip.so")
+MODEL_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libfrecsys_model.so")
 
 # Every symbol include/frecsys_hip.h declares (checked by the CPU tests).
 EXPORTS = (
@@ -36,6 +37,13 @@ EXPORTS = (
     "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset", "frecsys_debug_basis",
     "frecsys_eval_topk", "frecsys_train_stats", "frecsys_pp_set_rating_index",
     "frecsys_pp_predict", "frecsys_pp_step", "frecsys_debug_diag_factor",
+)
+
+# Every symbol include/frecsys_model.h declares.
+MODEL_EXPORTS = (
+    "frecsys_model_config_default", "frecsys_model_create", "frecsys_model_initialize",
+    "frecsys_model_train", "frecsys_model_context", "frecsys_model_mean_weight",
+    "frecsys_model_destroy", "frecsys_model_last_error",
 )
 
 
@@ -61,7 +69,23 @@ class _SolveParams(ctypes.Structure):
                 ("other_weight", ctypes.c_void_p)]
 
 
+class _ModelConfig(ctypes.Structure):
+    _fields_ = [("model_name", ctypes.c_char_p), ("dim", ctypes.c_int32),
+                ("l2_reg", ctypes.c_float), ("l2_reg_exp", ctypes.c_float),
+                ("uobs_weight", ctypes.c_float), ("stdev", ctypes.c_float),
+                ("alpha", ctypes.c_float), ("bandwidth", ctypes.c_float),
+                ("stepsize", ctypes.c_float), ("sampling_ratio", ctypes.c_float),
+                ("block_size", ctypes.c_int32), ("xi_iterations", ctypes.c_int32),
+                ("pd_iterations", ctypes.c_int32), ("use_epanechnikov", ctypes.c_int32),
+                ("use_snr", ctypes.c_int32), ("print_train_stats", ctypes.c_int32),
+                ("print_residual_stats", ctypes.c_int32), ("print_var_stats", ctypes.c_int32),
+                ("seed", ctypes.c_int64), ("device", ctypes.c_int32),
+                ("parity_quirks", ctypes.c_int32), ("world", ctypes.c_int32),
+                ("rank", ctypes.c_int32), ("comm_id", ctypes.c_void_p)]
+
+
 _lib = None
+_model_lib = None
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -112,6 +136,34 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
+def load_model_library(path: str = MODEL_LIB_PATH) -> ctypes.CDLL:
+    """Load libfrecsys_model.so (the C++ model classes behind a C-ABI)."""
+    global _model_lib
+    if _model_lib is not None:
+        return _model_lib
+    load_library()
+    if not os.path.exists(path):
+        raise FrecsysError(ERR_INVALID, f"{path} missing: run __graft_entry__.build() / make")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    sig = {
+        "frecsys_model_config_default": (None, [P]),
+        "frecsys_model_create": (ctypes.c_int, [P, P, P, I64, P]),
+        "frecsys_model_initialize": (ctypes.c_int, [P]),
+        "frecsys_model_train": (ctypes.c_int, [P, I32]),
+        "frecsys_model_context": (P, [P]),
+        "frecsys_model_mean_weight": (ctypes.c_float, [P]),
+        "frecsys_model_destroy": (None, [P]),
+        "frecsys_model_last_error": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _model_lib = lib
+    return lib
+
+
 def _ptr(a: Optional[np.ndarray]):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
@@ -151,8 +203,14 @@ class Context:
     """One device context (one GPU).  See include/frecsys_hip.h."""
 
     def __init__(self, dim: int, n_users: int, n_items: int, device: int = -1,
-                 parity_quirks: bool = True):
+                 parity_quirks: bool = True, _borrowed=None):
         self.lib = load_library()
+        self.owned = _borrowed is None
+        if _borrowed is not None:  # a model's context (frecsys_model_context)
+            self.h = ctypes.c_void_p(_borrowed)
+            self.dim = dim
+            self.n = {SIDE_USER: n_users, SIDE_ITEM: n_items, SIDE_EVAL: 0}
+            return
         cfg = _Config(dim, device, 1 if parity_quirks else 0, 0, n_users, n_items)
         h = ctypes.c_void_p()
         rc = self.lib.frecsys_ctx_create(ctypes.byref(cfg), ctypes.byref(h))
@@ -170,7 +228,8 @@ class Context:
 
     def close(self):
         if getattr(self, "h", None):
-            self.lib.frecsys_ctx_destroy(self.h)
+            if self.owned:
+                self.lib.frecsys_ctx_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -322,3 +381,67 @@ class Context:
         sb = np.zeros(Dp, dtype=np.float32)
         self._check(self.lib.frecsys_debug_basis(self.h, side, _ptr(q), _ptr(dg), _ptr(sb)))
         return q, dg, sb
+
+
+class Model:
+    """One model of include/frecsys_model.h: the run_model factory over the
+    C++ classes.  `users`, `items`: the training tuples in file order;
+    keyword arguments are the run_model flags (frecsys_model_config)."""
+
+    def __init__(self, model_name: str, users: np.ndarray, items: np.ndarray, **flags):
+        self.lib = load_model_library()
+        cfg = _ModelConfig()
+        self.lib.frecsys_model_config_default(ctypes.byref(cfg))
+        self._name = model_name.encode()
+        cfg.model_name = self._name
+        self._cid = None
+        for k, v in flags.items():
+            if k == "comm_id":
+                if v is not None:
+                    self._cid = (ctypes.c_uint8 * 128).from_buffer_copy(v)
+                    cfg.comm_id = ctypes.cast(self._cid, ctypes.c_void_p)
+                continue
+            if not hasattr(cfg, k):
+                raise TypeError(f"unknown model flag {k}")
+            setattr(cfg, k, int(v) if isinstance(v, bool) else v)
+        u = np.ascontiguousarray(users, dtype=np.int32)
+        it = np.ascontiguousarray(items, dtype=np.int32)
+        assert u.shape == it.shape
+        h = ctypes.c_void_p()
+        rc = self.lib.frecsys_model_create(ctypes.byref(cfg), _ptr(u), _ptr(it), len(u),
+                                           ctypes.byref(h))
+        if rc:
+            raise FrecsysError(rc, self.lib.frecsys_model_last_error().decode())
+        self.h = h
+        self.dim = cfg.dim
+        self.n_users = int(u.max()) + 1
+        self.n_items = int(it.max()) + 1
+
+    def initialize(self):
+        rc = self.lib.frecsys_model_initialize(self.h)
+        if rc:
+            raise FrecsysError(rc, self.lib.frecsys_model_last_error().decode())
+
+    def train(self, epochs: int = 1):
+        rc = self.lib.frecsys_model_train(self.h, epochs)
+        if rc:
+            raise FrecsysError(rc, self.lib.frecsys_model_last_error().decode())
+
+    def context(self) -> Context:
+        """The model's device context (borrowed: closing it is a no-op)."""
+        return Context(self.dim, self.n_users, self.n_items,
+                       _borrowed=self.lib.frecsys_model_context(self.h))
+
+    def mean_weight(self) -> float:
+        return float(self.lib.frecsys_model_mean_weight(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.frecsys_model_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -34,6 +34,8 @@ struct DeviceOptions {
   int world = 0;              // 0: from WORLD_SIZE (1 if unset)
   int rank = -1;              // -1: from RANK
   std::string comm_file;      // RCCL id rendezvous file for world > 1
+  bool has_comm_id = false;   // comm_id given by the caller (e.g. exchanged over
+  std::array<uint8_t, 128> comm_id{};  // torch.distributed): no file rendezvous
 
   static DeviceOptions FromEnv() {
     DeviceOptions o;
@@ -197,6 +199,10 @@ class DeviceContext {
     check(frecsys_load_csr(ctx_, side, rows, ptr.data(), c.col.data()), "load_csr");
   }
   void comm_init(const DeviceOptions& o) {
+    if (o.has_comm_id) {
+      check(frecsys_comm_init(ctx_, world_, rank_, o.comm_id.data()), "comm_init");
+      return;
+    }
     std::string path = o.comm_file;
     if (path.empty()) {
       const char* f = getenv("FRECSYS_COMM_FILE");

@@ -19,12 +19,7 @@
 #include <string>
 #include <sys/stat.h>
 
-#include "frecsys/cvar_mf.h"
-#include "frecsys/erm_mf.h"
-#include "frecsys/ials.h"
-#include "frecsys/ialspp.h"
-#include "frecsys/safer2.h"
-#include "frecsys/safer2pp.h"
+#include "frecsys/factory.h"
 
 namespace {
 
@@ -109,47 +104,29 @@ void evaluate(int epoch, F recommender, frecsys::Dataset& exclude, frecsys::Data
   metrics.show();
 }
 
-frecsys::Recommender* get_model(const std::string& name, int num_users, int num_items,
-                                const Flags& a, const frecsys::DeviceOptions& o) {
-  frecsys::Recommender* r = nullptr;
-  if (name == "ials") {
-    r = new frecsys::IALSRecommender(a.i("--dim"), num_users, num_items, a.f("--l2_reg"),
-                                     a.f("--l2_reg_exp"), a.f("--uobs_weight"), a.f("--stdev"),
-                                     a.f("--alpha"), a.b("--use_cg"),
-                                     a.f("--cg_error_tolerance"), a.i("--cg_max_iterations"), o);
-  } else if (name == "ialspp") {
-    r = new frecsys::IALSppRecommender(a.i("--dim"), num_users, num_items, a.f("--l2_reg"),
-                                       a.f("--l2_reg_exp"), a.f("--uobs_weight"),
-                                       a.f("--stdev"), a.f("--alpha"), a.i("--block_size"), o);
-  } else if (name == "safer2") {
-    r = new frecsys::SAFER2Recommender(
-        a.i("--dim"), num_users, num_items, a.f("--l2_reg"), a.f("--uobs_weight"),
-        a.f("--bandwidth"), a.f("--alpha"), a.f("--stdev"), a.i("--xi_iterations"),
-        a.i("--pd_iterations"), a.b("--use_epanechnikov"), a.b("--use_snr"),
-        a.f("--sampling_ratio"), a.b("--use_cg"), a.f("--cg_error_tolerance"),
-        a.i("--cg_max_iterations"), o);
-  } else if (name == "safer2pp") {
-    r = new frecsys::SAFER2ppRecommender(
-        a.i("--dim"), num_users, num_items, a.f("--l2_reg"), a.f("--uobs_weight"),
-        a.f("--bandwidth"), a.f("--alpha"), a.f("--stdev"), a.i("--xi_iterations"),
-        a.i("--pd_iterations"), a.b("--use_epanechnikov"), a.b("--use_snr"),
-        a.f("--sampling_ratio"), a.i("--block_size"), o);
-  } else if (name == "erm_mf") {
-    r = new frecsys::ERMMFRecommender(a.i("--dim"), num_users, num_items, a.f("--l2_reg"),
-                                      a.f("--uobs_weight"), a.f("--stdev"), a.f("--alpha"),
-                                      a.b("--use_cg"), a.f("--cg_error_tolerance"),
-                                      a.i("--cg_max_iterations"), o);
-  } else if (name == "cvar_mf") {
-    r = new frecsys::CVaRMFRecommender(a.i("--dim"), num_users, num_items, a.f("--l2_reg"),
-                                       a.f("--uobs_weight"), a.f("--alpha"), a.f("--stepsize"),
-                                       a.f("--stdev"), o);
-  } else {
-    LOG(FATAL) << "model " << name << " is not part of this build";
-  }
-  r->SetPrintResidualStats(a.b("--print_residual_stats"));
-  r->SetPrintVarStats(a.b("--print_var_stats"));
-  r->SetPrintTrainStats(a.b("--print_train_stats"));
-  return r;
+frecsys::ModelParams model_params(const Flags& a) {
+  frecsys::ModelParams p;
+  p.dim = a.i("--dim");
+  p.l2_reg = a.f("--l2_reg");
+  p.l2_reg_exp = a.f("--l2_reg_exp");
+  p.uobs_weight = a.f("--uobs_weight");
+  p.stdev = a.f("--stdev");
+  p.alpha = a.f("--alpha");
+  p.bandwidth = a.f("--bandwidth");
+  p.stepsize = a.f("--stepsize");
+  p.sampling_ratio = a.f("--sampling_ratio");
+  p.cg_error_tolerance = a.f("--cg_error_tolerance");
+  p.cg_max_iterations = a.i("--cg_max_iterations");
+  p.use_cg = a.b("--use_cg");
+  p.block_size = a.i("--block_size");
+  p.xi_iterations = a.i("--xi_iterations");
+  p.pd_iterations = a.i("--pd_iterations");
+  p.use_epanechnikov = a.b("--use_epanechnikov");
+  p.use_snr = a.b("--use_snr");
+  p.print_train_stats = a.b("--print_train_stats");
+  p.print_residual_stats = a.b("--print_residual_stats");
+  p.print_var_stats = a.b("--print_var_stats");
+  return p;
 }
 
 }  // namespace
@@ -190,8 +167,7 @@ int main(int argc, char* argv[]) {
 
   std::string model_name = app.str("--model_name");
   std::transform(model_name.begin(), model_name.end(), model_name.begin(), ::tolower);
-  static const char* kModels[] = {"ials", "ialspp", "safer2", "safer2pp", "cvar_mf", "erm_mf"};
-  if (std::find(std::begin(kModels), std::end(kModels), model_name) == std::end(kModels)) {
+  if (!frecsys::IsKnownModel(model_name)) {
     fprintf(stderr, "--model_name: %s not in {ials,ialspp,safer2,safer2pp,cvar_mf,erm_mf}\n",
             model_name.c_str());
     return 105;
@@ -212,15 +188,11 @@ int main(int argc, char* argv[]) {
   opts.seed = std::atoll(app.str("--seed").c_str());
   opts.device = app.i("--device");
   opts.parity_quirks = app.b("--parity_quirks");
-  frecsys::Recommender* recommender =
-      get_model(model_name, train.max_user() + 1, train.max_item() + 1, app, opts);
+  frecsys::Recommender* recommender = frecsys::MakeRecommender(
+      model_name, train.max_user() + 1, train.max_item() + 1, model_params(app), opts);
   setbuf(stdout, NULL);
 
-  if (model_name == "cvar_mf") ((frecsys::CVaRMFRecommender*)recommender)->Initialize(train);
-  if (model_name == "safer2") ((frecsys::SAFER2Recommender*)recommender)->Initialize(train);
-  if (model_name == "safer2pp")
-    ((frecsys::SAFER2ppRecommender*)recommender)->Initialize(train);
-  if (model_name == "erm_mf") ((frecsys::ERMMFRecommender*)recommender)->Initialize(train);
+  frecsys::InitializeRecommender(model_name, recommender, train);  // run_model.cc:246-257
   const int epochs = app.i("--epoch");
   const bool print_eval = app.b("--print_evaluation_stats");
   for (int epoch = 0; epoch < epochs; ++epoch) {

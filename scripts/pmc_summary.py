@@ -1,10 +1,21 @@
-"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into per-launch
-HBM traffic (bytes) per kernel, with the gfx950 correction of
-/opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB, = TCC_EA0_RDREQ
-x 64 B) reads half the bytes of wide coalesced streams -> x2; WRITE_SIZE is
-taken as is.  Usage: pmc_summary.py <fetch.csv> <write.csv> <out.json>"""
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of one bench.py
+workload into per-launch fabric traffic (bytes) per kernel, and the traffic
+of the workload's roofline kernel per d-space call (the unit bench.py's
+`roofline.achieved` is per).
+
+gfx950 correction (/opt/skills/guides/MI355X_MICROARCH.md, HBM section):
+FETCH_SIZE (KiB, = TCC_EA0_RDREQ x 64 B) reports half the bytes of 16-B/lane
+streaming reads -> x2; WRITE_SIZE as is.  The solve kernels gather 4-B/lane
+(one float per lane, 64 lanes = one 256-B row segment): that width is not
+calibrated by the guide, so both the raw and the x2 figures are kept.
+
+Usage: pmc_summary.py <workload> <fetch.csv> <write.csv> <epochs> <out.json> [<merge.json>]
+  epochs: Train() epochs the pass ran (warmup + steps); the d-space solve runs
+  once per half-step, 2 per epoch.
+"""
 import csv
 import json
+import os
 import sys
 
 
@@ -13,34 +24,57 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"]
-        out.setdefault(name, []).append(float(r["Counter_Value"]) * 1024.0)
+        out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]) * 1024.0)
     return out
 
 
-fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
-write = per_kernel(sys.argv[2], "WRITE_SIZE")
-summary = {"correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1; bytes per launch",
-           "kernels": {}}
-for name in sorted(set(fetch) | set(write)):
-    f = fetch.get(name, [])
-    w = write.get(name, [])
-    summary["kernels"][name] = {
-        "launches": max(len(f), len(w)),
-        "fetch_bytes_per_launch_raw": f,
-        "fetch_bytes_per_launch": [2.0 * x for x in f],
-        "write_bytes_per_launch": w,
-    }
-# the d-space solve (roofline kernel): launches alternate user, item in
-# every bench epoch (warmup included); averaged over all launches
-for name, v in summary["kernels"].items():
-    if "solve_tiled_kernel<8, false" in name:  # <8, false> / <8, false, BF>
-        tot = [a + b for a, b in zip(v["fetch_bytes_per_launch"], v["write_bytes_per_launch"])]
-        summary["dspace_traffic_bytes"] = sum(tot) / max(1, len(tot))
-        summary["dspace_user_traffic_bytes"] = sum(tot[0::2]) / max(1, len(tot[0::2]))
-        summary["dspace_item_traffic_bytes"] = sum(tot[1::2]) / max(1, len(tot[1::2]))
-json.dump(summary, open(sys.argv[3], "w"), indent=1)
-print(json.dumps({k: {"fetch_GB": [round(x / 1e9, 3) for x in v["fetch_bytes_per_launch"]],
-                      "write_GB": [round(x / 1e9, 3) for x in v["write_bytes_per_launch"]]}
-                  for k, v in summary["kernels"].items()
-                  if "solve" in k or "loss" in k or "dual" in k}, indent=1))
+def dominant(name, workload):
+    if "d512" in workload or "d1024" in workload:
+        return "wide_syrk_kernel<1" in name or "wide_chol_kernel" in name
+    return "solve_tiled_kernel<8, false" in name
+
+
+def main():
+    workload, fpath, wpath, epochs, out = sys.argv[1:6]
+    merge = sys.argv[6] if len(sys.argv) > 6 else None
+    calls = 2 * int(epochs)
+    fetch = per_kernel(fpath, "FETCH_SIZE")
+    write = per_kernel(wpath, "WRITE_SIZE")
+    summary = {"workload": workload, "epochs": int(epochs),
+               "correction": "FETCH_SIZE x2 (gfx950 16-B/lane calibration; 4-B/lane gathers "
+                             "uncalibrated, raw kept), WRITE_SIZE x1",
+               "kernels": {}}
+    dom_f = dom_f_raw = dom_w = 0.0
+    for name in sorted(set(fetch) | set(write)):
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        summary["kernels"][name] = {
+            "launches": max(len(f), len(w)),
+            "fetch_bytes_per_launch_raw": sum(f) / max(1, len(f)),
+            "fetch_bytes_per_launch": 2.0 * sum(f) / max(1, len(f)),
+            "write_bytes_per_launch": sum(w) / max(1, len(w)),
+        }
+        if dominant(name, workload):
+            dom_f += 2.0 * sum(f)
+            dom_f_raw += sum(f)
+            dom_w += sum(w)
+    summary["dominant_traffic_bytes"] = (dom_f + dom_w) / calls
+    summary["dominant_traffic_bytes_raw_fetch"] = (dom_f_raw + dom_w) / calls
+    json.dump(summary, open(out, "w"), indent=1)
+    if merge:
+        js = json.load(open(merge)) if os.path.exists(merge) else {}
+        js.setdefault("workloads", {})[workload] = {
+            "dominant_traffic_bytes": summary["dominant_traffic_bytes"],
+            "dominant_traffic_bytes_raw_fetch": summary["dominant_traffic_bytes_raw_fetch"]}
+        js["source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --workload <w> "
+                        "(profiles/<round>/pmc_<w>.json): fabric-side bytes (L2 misses incl. "
+                        "Infinity-Cache hits) of the roofline kernel per d-space call, FETCH x2")
+        json.dump(js, open(merge, "w"), indent=1)
+    print(json.dumps({k: {"fetch_GB": round(v["fetch_bytes_per_launch"] / 1e9, 4),
+                          "write_GB": round(v["write_bytes_per_launch"] / 1e9, 4),
+                          "launches": v["launches"]}
+                      for k, v in summary["kernels"].items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,13 +1,31 @@
 #!/bin/bash
-# Measurement pass for the round: bench line + rocprofv3 kernel stats + PMC
-# traffic passes (separate runs, never combined with tracing domains).
+# Measurement pass for the round (run on the GPU box through gpurun):
+#   1. the default bench line (headline + extra workloads, CPU baselines)
+#   2. per workload: rocprofv3 kernel stats of the same command, then the
+#      FETCH_SIZE and WRITE_SIZE passes (separate runs, no tracing domains),
+#      summarised into profiles/latest_pmc.json by scripts/pmc_summary.py
+#   3. serialised streams (FRECSYS_DUAL_SERIAL=1): kernel stats + one SQ pass
+#      (MFMA busy, wait/issue stalls) of the headline workload
+# Usage: profile_round.sh <outdir under gpurun_out> [workloads...]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/$1
+shift
+WL=${*:-ials_ml20m_d256 safer2_ml20m_d256 ials_msd_d512}
 mkdir -p $OUT
-timeout -k 10 400 python bench.py --steps 5 --warmup 2 > $OUT/bench.json 2> $OUT/bench.err || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 > $OUT/trace.log 2>&1 || exit 2
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 > $OUT/pmc_fetch.log 2>&1 || exit 3
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --cpu-seconds 0 > $OUT/pmc_write.log 2>&1 || exit 4
+timeout -k 10 420 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; exit 1; }
+echo "bench ok"
+for w in $WL; do
+  ARGS="--workload $w --extras= --steps 3 --warmup 1 --cpu-seconds 0 --quiet"
+  timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/trace_$w -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace_$w.log 2>&1 || { echo trace $w failed; exit 2; }
+  PARGS="--workload $w --extras= --steps 1 --warmup 1 --cpu-seconds 0 --quiet"
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch_$w -o run --output-format csv -- python3 bench.py $PARGS > $OUT/fetch_$w.log 2>&1 || { echo fetch $w failed; exit 3; }
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/write_$w -o run --output-format csv -- python3 bench.py $PARGS > $OUT/write_$w.log 2>&1 || { echo write $w failed; exit 4; }
+  python3 scripts/pmc_summary.py $w $(ls $OUT/fetch_$w/*/*counter_collection.csv | head -1) $(ls $OUT/write_$w/*/*counter_collection.csv | head -1) 2 $OUT/pmc_$w.json $OUT/latest_pmc.json > $OUT/pmc_$w.txt || { echo summary $w failed; exit 5; }
+  echo "$w ok"
+done
+SARGS="--workload ials_ml20m_d256 --extras= --steps 2 --warmup 1 --cpu-seconds 0 --quiet --allow-env"
+FRECSYS_DUAL_SERIAL=1 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/trace_serial -o run --output-format csv -- python3 bench.py $SARGS > $OUT/trace_serial.log 2>&1 || { echo serial trace failed; exit 6; }
+FRECSYS_DUAL_SERIAL=1 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/sq_serial -o run --output-format csv -- python3 bench.py $SARGS > $OUT/sq_serial.log 2>&1 || { echo sq pass failed; exit 7; }
 echo done

@@ -1,6 +1,7 @@
 """C-ABI checks that need no GPU: the library loads, exports every symbol
 include/frecsys_hip.h declares, its host-only helpers work, and compute entry
 points fail loudly (no CPU fallback) when no device is visible."""
+import ctypes
 import os
 import re
 import subprocess
@@ -12,10 +13,11 @@ import frecsys_hip as fh
 from conftest import ROOT
 
 HEADER = os.path.join(ROOT, "include", "frecsys_hip.h")
+MODEL_HEADER = os.path.join(ROOT, "include", "frecsys_model.h")
 
 
-def _declared():
-    txt = open(HEADER).read()
+def _declared(header=HEADER):
+    txt = open(header).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(frecsys_[a-z_0-9]+)\s*\(", txt)))
 
@@ -78,3 +80,48 @@ def test_context_without_device_fails_loudly():
     with pytest.raises(fh.FrecsysError) as ei:
         fh.Context(16, 10, 10)
     assert ei.value.code in (fh.ERR_NO_DEVICE, fh.ERR_HIP)
+
+
+def test_model_library_exports_every_declared_symbol():
+    names = _declared(MODEL_HEADER)
+    assert set(names) == set(fh.MODEL_EXPORTS), set(names) ^ set(fh.MODEL_EXPORTS)
+    lib = fh.load_model_library()
+    out = subprocess.run(["nm", "-D", "--defined-only", fh.MODEL_LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (frecsys_\w+)", out))
+    for name in names:
+        assert name in exported, name
+        assert getattr(lib, name) is not None
+
+
+def test_model_config_defaults_are_run_model_flags():
+    lib = fh.load_model_library()
+    cfg = fh._ModelConfig()
+    lib.frecsys_model_config_default(ctypes.byref(cfg))
+    # run_model.cc:129-230
+    assert (cfg.dim, cfg.block_size, cfg.xi_iterations, cfg.pd_iterations) == (8, 64, 5, 1)
+    assert np.float32(cfg.l2_reg) == np.float32(0.002) and cfg.l2_reg_exp == 1.0
+    assert np.float32(cfg.uobs_weight) == np.float32(0.1)
+    assert np.float32(cfg.alpha) == np.float32(0.3) and cfg.bandwidth == 1.0
+    assert cfg.print_train_stats == 1 and cfg.use_snr == 0 and cfg.seed == -1
+
+
+def test_model_create_rejects_bad_arguments():
+    u = np.array([0, 1, 1], np.int32)
+    i = np.array([0, 0, 1], np.int32)
+    with pytest.raises(fh.FrecsysError) as ei:
+        fh.Model("als_unknown", u, i, dim=8)
+    assert ei.value.code == fh.ERR_INVALID
+    with pytest.raises(fh.FrecsysError) as ei:
+        fh.Model("ials", u, i, dim=2048)
+    assert ei.value.code == fh.ERR_UNSUPPORTED
+    with pytest.raises(fh.FrecsysError) as ei:
+        fh.Model("ials", np.array([0, -1], np.int32), np.array([0, 0], np.int32), dim=8)
+    assert ei.value.code == fh.ERR_INVALID
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible here")
+def test_model_without_device_fails_loudly():
+    with pytest.raises(fh.FrecsysError) as ei:
+        fh.Model("ials", np.array([0, 1], np.int32), np.array([1, 0], np.int32), dim=8)
+    assert ei.value.code == fh.ERR_NO_DEVICE
