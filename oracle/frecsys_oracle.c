@@ -237,24 +237,39 @@ static void add_lower(float* A, const float* T, int d) {
 }
 
 /* LLT<MatrixXf, Lower> (ials.h:140): reads the lower triangle only.
- * Left-looking dot-product form, the form of Eigen's unblocked kernel
- * (Eigen/src/Cholesky/LLT.h llt_inplace::unblocked). L overwrites lower. */
+ * Every element sees the arithmetic of the left-looking dot-product form of
+ * Eigen's unblocked kernel (Eigen/src/Cholesky/LLT.h llt_inplace::unblocked):
+ * L(i,j) = (A(i,j) - L(i,0)L(j,0) - L(i,1)L(j,1) - ...) / L(j,j), the
+ * subtractions in ascending k, no FMA contraction (-std=c11).  It is run
+ * right-looking -- column j's products are subtracted from the trailing
+ * lower triangle as soon as column j is final -- which performs the same
+ * subtractions in the same order per element (bit-identical results) with
+ * a unit-stride inner loop the compiler vectorises.  L overwrites lower. */
 static int cholesky_lower(float* A, int d) {
+  float* c = (float*)malloc(sizeof(float) * (size_t)(d > 0 ? d : 1));
+  int rc = 0;
   for (int j = 0; j < d; ++j) {
     float* Lj = A + (size_t)j * d;
-    float s = Lj[j];
-    for (int k = 0; k < j; ++k) s -= Lj[k] * Lj[k];
-    if (!(s > 0.0f)) return -1;
+    const float s = Lj[j];
+    if (!(s > 0.0f)) {
+      rc = -1;
+      break;
+    }
     const float ljj = sqrtf(s);
     Lj[j] = ljj;
     for (int i = j + 1; i < d; ++i) {
       float* Li = A + (size_t)i * d;
-      float t = Li[j];
-      for (int k = 0; k < j; ++k) t -= Li[k] * Lj[k];
-      Li[j] = t / ljj;
+      Li[j] = Li[j] / ljj;
+      c[i] = Li[j];
+    }
+    for (int i = j + 1; i < d; ++i) {
+      float* Li = A + (size_t)i * d;
+      const float lij = c[i];
+      for (int k = j + 1; k <= i; ++k) Li[k] -= lij * c[k];
     }
   }
-  return 0;
+  free(c);
+  return rc;
 }
 
 /* cholesky.solve(rhs): L y = b, L^T x = y. */

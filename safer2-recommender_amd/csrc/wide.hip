@@ -51,6 +51,7 @@ namespace {
 constexpr int WB = 128;    // block-pair edge
 constexpr int WR = 16;     // rows per staged chunk
 constexpr int WRING = 4;   // row-id ring slots
+constexpr int WFLUSH = 256; // chunks (x WR rows) per accumulator flush
 constexpr int kWideMaxBlocks = 64;
 
 __device__ __forceinline__ void pair_of(int pidx, int& BI, int& BJ) {
@@ -90,7 +91,7 @@ __device__ __forceinline__ bool xcd_unit(int P, int64_t n_units, int64_t& unit, 
 // MODE 0: partial Gramian of the unit's rows [r0, r1) (operand weight g.w);
 // MODE 1: assembly of entity order[pos0 + unit] into its workspace slot.
 template <int MODE>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 3)  // 3 waves per SIMD (<= 168 registers)
     wide_syrk_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws,
                      int64_t n_units) {
   __shared__ __attribute__((aligned(16))) float xa[2][WR * WB];
@@ -226,21 +227,40 @@ __global__ void __launch_bounds__(256)
                         a.lambda_is_reg);
   }
   const float gscale = kind == KIND_IALS ? a.w : (is_u_kind(kind) ? hf * a.w : a.w);
+  // Two-level accumulation: the MFMAs accumulate at most WFLUSH chunks of
+  // rows from zero, then the chunk sum is added into the unit's own output
+  // tiles (workspace slot / Gramian partial; this workgroup is their only
+  // writer, so no atomics).  One MFMA accumulator over a ~190K-row history
+  // (MSD head items) drifts by ~2e-4 relative; chunk sums keep the error at
+  // the level of a WFLUSH * WR-row sum.  The G part of A joins in the epilogue.
+  float* const otile0 = MODE == 0 ? g.partials + unit * NT * 1024
+                                  : ws + unit * ((int64_t)NT * 1024 + Dp);
+  auto otile = [&](int j) {
+    return otile0 + (int64_t)tidx(4 * BI + wave, 4 * BJ + j) * 1024;
+  };
+  bool flushed = false;
   f32x16 acc[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    acc[j] = f32x16{0.f};
-    if (MODE == 1 && !grad && (!dgp || j <= wave)) {
+  for (int j = 0; j < 4; ++j) acc[j] = f32x16{0.f};
+  float bacc = 0.0f, btot = 0.0f;
+  auto flush = [&]() {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int gi = WB * BI + 32 * wave + acc_row(q, hi), gj = WB * BJ + 32 * j + lo;
-        float v = gscale * a.G[(int64_t)gi * Dp + gj];
-        if (kind == KIND_IALS && gi == gj) v += lam;
-        acc[j][q] = v;
+    for (int j = 0; j < 4; ++j) {
+      if (!dgp || j <= wave) {  // wave-uniform
+        float* t = otile(j);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          float* p = t + acc_row(q, hi) * 32 + lo;
+          *p = flushed ? *p + acc[j][q] : acc[j][q];
+        }
       }
+      acc[j] = f32x16{0.f};
+      __builtin_amdgcn_sched_barrier(0);  // one tile's 16 values live at a time
     }
-  }
-  float bacc = 0.0f;
+    btot += bacc;
+    bacc = 0.0f;
+    flushed = true;
+  };
   lds_barrier();
   if (nchunks > 0) {
     load_data(0);
@@ -273,9 +293,36 @@ __global__ void __launch_bounds__(256)
 #pragma unroll 4
       for (int r = 0; r < WR; ++r) bacc += ring_bw[slot * WR + r] * sa_[r * WB + tid];
     }
+    if ((c + 1) % WFLUSH == 0 && more) flush();  // block-uniform
     if (more) store_stage(buf ^ 1, c + 1);
     if (ring_more) ring_store(c + 2, nid, nsa, nbw);
     lds_barrier();
+  }
+  if (flushed) {  // fold the stored chunk sums back in (same thread wrote them)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!dgp || j <= wave) {
+        const float* t = otile(j);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[j][q] += t[acc_row(q, hi) * 32 + lo];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  bacc += btot;
+  if (MODE == 1 && !grad) {  // G part of A (as solve.hip): iALS w*G + lam*I, U h*w*G, V w*G
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!dgp || j <= wave) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int gi = WB * BI + 32 * wave + acc_row(q, hi), gj = WB * BJ + 32 * j + lo;
+          float v = gscale * a.G[(int64_t)gi * Dp + gj];
+          if (kind == KIND_IALS && gi == gj) v += lam;
+          acc[j][q] += v;
+        }
+      }
+    }
   }
 
   if (MODE == 0) {

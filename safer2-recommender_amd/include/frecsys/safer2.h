@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "frecsys/model_base.h"
+#include "frecsys/parallel.h"
 
 namespace frecsys {
 namespace quantile {
@@ -64,28 +65,37 @@ struct Smoother {
   // and each `r.unaryExpr(lambda).mean()` is Eigen's reduction of an
   // expression without packet access (Redux.h DefaultTraversal): a
   // sequential float sum from the first element, then / float(n).
+  // The per-sample terms are independent and are computed by the host
+  // thread pool into scratch arrays; the three sums then run serially in
+  // index order, so the result is bit-identical to the serial loop.
   std::tuple<float, float, float> Evaluate(float xi, const float* loss, int64_t n) const {
+    tc.resize((size_t)n);
+    tk.resize((size_t)n);
+    tl.resize((size_t)n);
+    ThreadPool::Get().ParallelFor(n, 2048, [&](int64_t lo, int64_t hi) {
+      for (int64_t i = lo; i < hi; ++i) {
+        const float u = loss[i] - xi;
+        if (epan) {
+          tc[i] = epanechnikov_kernel_cdf(-u, bandwidth);
+          tk[i] = epanechnikov_kernel(-u, bandwidth);
+          tl[i] = epanechnikov_loss(u, bandwidth, alpha);
+        } else {
+          tc[i] = gaussian_kernel_cdf(-u, bandwidth);
+          tk[i] = gaussian_kernel(-u, bandwidth);
+          tl[i] = gaussian_loss(u, bandwidth, alpha);
+        }
+      }
+    });
     float sc = 0, sk = 0, sl = 0;
     for (int64_t i = 0; i < n; ++i) {
-      const float u = loss[i] - xi;
-      float c, k, l;
-      if (epan) {
-        c = epanechnikov_kernel_cdf(-u, bandwidth);
-        k = epanechnikov_kernel(-u, bandwidth);
-        l = epanechnikov_loss(u, bandwidth, alpha);
-      } else {
-        c = gaussian_kernel_cdf(-u, bandwidth);
-        k = gaussian_kernel(-u, bandwidth);
-        l = gaussian_loss(u, bandwidth, alpha);
-      }
       if (i == 0) {
-        sc = c;
-        sk = k;
-        sl = l;
+        sc = tc[i];
+        sk = tk[i];
+        sl = tl[i];
       } else {
-        sc += c;
-        sk += k;
-        sl += l;
+        sc += tc[i];
+        sk += tk[i];
+        sl += tl[i];
       }
     }
     const float fn = (float)n;
@@ -94,6 +104,7 @@ struct Smoother {
     const float value = (sl / fn) / alpha;
     return {value, grad, H};
   }
+  mutable std::vector<float> tc, tk, tl;  // per-sample scratch
   // ComputeXiDirection (safer2.h:692-712): Newton step with Armijo
   // backtracking (c = 1e-4, <= 32 halvings, gradient at the trial point).
   float Direction(float xi, const float* loss, int64_t n) const {
@@ -249,8 +260,11 @@ class SAFER2Recommender : public detail::DeviceModel {
   // ComputeUserWeights (safer2.h:745-794): only users with a history.
   void ComputeUserWeights(const Dataset& data) {
     const Csr& uc = data.user_csr();
-    for (int64_t u = 0; u < uc.rows() && u < num_users_; ++u)
-      if (uc.len(u)) dual_weight_[u] = smoother_.Weight(user_loss_[u], prev_xi_);
+    const int64_t n = std::min<int64_t>(uc.rows(), num_users_);
+    ThreadPool::Get().ParallelFor(n, 4096, [&](int64_t lo, int64_t hi) {
+      for (int64_t u = lo; u < hi; ++u)
+        if (uc.len(u)) dual_weight_[u] = smoother_.Weight(user_loss_[u], prev_xi_);
+    });
   }
 
   // StepV (safer2.h:493-555).

@@ -22,7 +22,7 @@ for w in $WL; do
   PARGS="--workload $w --extras= --steps 1 --warmup 1 --cpu-seconds 0 --quiet"
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch_$w -o run --output-format csv -- python3 bench.py $PARGS > $OUT/fetch_$w.log 2>&1 || { echo fetch $w failed; exit 3; }
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d $OUT/write_$w -o run --output-format csv -- python3 bench.py $PARGS > $OUT/write_$w.log 2>&1 || { echo write $w failed; exit 4; }
-  python3 scripts/pmc_summary.py $w $(ls $OUT/fetch_$w/*/*counter_collection.csv | head -1) $(ls $OUT/write_$w/*/*counter_collection.csv | head -1) 2 $OUT/pmc_$w.json $OUT/latest_pmc.json > $OUT/pmc_$w.txt || { echo summary $w failed; exit 5; }
+  python3 scripts/pmc_summary.py $w $(ls $OUT/fetch_$w/*counter_collection.csv $OUT/fetch_$w/*/*counter_collection.csv 2>/dev/null | head -1) $(ls $OUT/write_$w/*counter_collection.csv $OUT/write_$w/*/*counter_collection.csv 2>/dev/null | head -1) 2 $OUT/pmc_$w.json $OUT/latest_pmc.json > $OUT/pmc_$w.txt || { echo summary $w failed; exit 5; }
   echo "$w ok"
 done
 SARGS="--workload ials_ml20m_d256 --extras= --steps 2 --warmup 1 --cpu-seconds 0 --quiet --allow-env"

@@ -113,8 +113,9 @@ def test_train_trajectory_matches_oracle(tmp_path, ml1m_csr, case, dim):
            u_max=float(eu.max()), u_p999=float(np.percentile(eu, 99.9)),
            v_max=float(ev.max()), v_p999=float(np.percentile(ev, 99.9)),
            u_over_1e4=int((eu > 1e-4).sum()), v_over_1e4=int((ev > 1e-4).sum()))
-    assert np.percentile(ev, 99.9) < 1e-4 and ev.max() < 1e-3, (ev.max(), np.percentile(ev, 99.9))
-    assert np.percentile(eu, 99.9) < 1e-4 and eu.max() < 1e-3, (eu.max(), np.percentile(eu, 99.9))
+    # north_star's bar on every row (observed maxima: gpurun_out/parity_report.jsonl)
+    assert ev.max() < 1e-4, (ev.max(), np.percentile(ev, 99.9))
+    assert eu.max() < 1e-4, (eu.max(), np.percentile(eu, 99.9))
     if oid != O.MODEL_IALS:
         np.testing.assert_allclose(loss, lo, rtol=1e-3, atol=1e-6)
     if oid in (O.MODEL_SAFER2, O.MODEL_CVAR):
