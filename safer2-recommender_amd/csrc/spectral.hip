@@ -16,18 +16,14 @@
 //                  slabs; optional entity list for gather/scatter.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace frecsys_hip {
 
 namespace {
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
 
 // Sum over a full wave with DPP row ops (no LDS round trips); every lane
 // gets the total.
@@ -52,59 +48,104 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
-// Householder tridiagonalisation, register-resident: the 1024 threads hold
-// the FULL symmetric matrix (zero-padded to 256) as 8 x 8 blocks; thread
-// t owns block row bi = t & 31 of block column bj = t >> 5, so the owners
-// of one block column are 32 lanes of one wave.  Step k (LAPACK sytd2,
-// lower): the wave owning column k forms the reflector v (v_{k+1} = 1),
-// tau, beta right after its own update of step k-1 and publishes v;
-// p = tau A v (8x8 block products, partial row sums reduced through LDS,
-// v^T A v reduced alongside for K); w = p - K v, K = (tau/2) v.p;
-// A -= v w^T + w v^T on the whole matrix -- v is zero on rows <= k, so this
-// is exactly H A H and the trailing block sees the textbook arithmetic.
-// Three barriers per step.
-__global__ void __launch_bounds__(1024)
+// DPP row operations (within 16-lane rows).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int DPP_XOR1 = 0xB1;         // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;         // quad_perm [2,3,0,1]
+constexpr int DPP_ROR8 = 0x128;        // row_ror:8 (= lane ^ 8 in a 16-lane row)
+constexpr int DPP_ROR4 = 0x124;
+constexpr int DPP_HALF_MIRROR = 0x141; // lane i <- 7 - i within each 8 (flips bit 2)
+// Sum over a 16-lane DPP row; every lane of the row gets it.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp<DPP_ROR8>(v);
+  v += dpp<DPP_ROR4>(v);
+  v += dpp<DPP_XOR2>(v);
+  v += dpp<DPP_XOR1>(v);
+  return v;
+}
+
+// Per-phase cycle counters of tridiag_kernel, per wave (diagnostics:
+// scripts/micro/tridiag_prof.hip builds with -DFRECSYS_TRIDIAG_PROF).
+#ifdef FRECSYS_TRIDIAG_PROF
+__device__ unsigned long long g_tri_prof[16][8];  // [wave][phase]
+#define TRI_PROF_DECL unsigned long long tp_last = clock64(), tp_acc[6] = {0, 0, 0, 0, 0, 0};
+#define TRI_PROF_MARK(i)                      \
+  {                                           \
+    const unsigned long long t_ = clock64();  \
+    tp_acc[i] += t_ - tp_last;                \
+    tp_last = t_;                             \
+  }
+#define TRI_PROF_FLUSH \
+  if (lane == 0)       \
+    for (int i = 0; i < 6; ++i) g_tri_prof[wave][i] = tp_acc[i];
+#else
+#define TRI_PROF_DECL
+#define TRI_PROF_MARK(i)
+#define TRI_PROF_FLUSH
+#endif
+
+// Householder tridiagonalisation (LAPACK sytd2 conventions, v(k+1) = 1),
+// register-resident in one workgroup of 8 waves (2 per SIMD, so 256
+// registers per lane): the symmetric matrix (zero-padded to 256) as 8 x 16
+// blocks, thread (wave w, lane l) owning rows 8 (4w + l/16) .. +7 and
+// columns 16 (l % 16) .. +15 -- each group of 8 rows lives in one 16-lane DPP
+// row.  Every reduction of a step is a handful of DPP ops inside one wave:
+//  * p = tau A v: each thread's 8 row partials are reduce-scattered over its
+//    16 lanes (row_ror:8, row_half_mirror, quad perms), one LDS store per row;
+//  * reflector k+1 is formed from ROW k+1 of the (symmetric) matrix, held by
+//    one 16-lane group (norm, x0, diagonal by 16-lane sums), right after that
+//    wave has updated this one row -- its latency hides under the rest of
+//    the update.
+// Column pairs run on v_pk_fma_f32.  Two LDS-only barriers per step (p
+// published, v published): the reflector's global stores (Vh, T, tau) are
+// never waited on inside the loop.  K = (tau/2) v.p is formed by every wave
+// from the published p.  Step k only needs the trailing block
+// [k+1:, k+1:], so waves whose 32 rows are all <= k skip its arithmetic.
+__global__ void __launch_bounds__(512)
     tridiag_kernel(const float* __restrict__ G, int n, float* tdiag, float* toff, float* Vh,
                    float* tau_out) {
-  __shared__ float vs[2][256];
-  __shared__ float ps[256];
-  __shared__ float part[32 * 257];
-  __shared__ float red[2][16];
+  typedef float f2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 operands
+  __shared__ __attribute__((aligned(16))) float vs[2][256];
+  __shared__ __attribute__((aligned(16))) float ps[256];
   __shared__ float tsh[2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int bi = tid & 31, bj = tid >> 5;
-  const int r0 = 8 * bi, c0 = 8 * bj;
-  float A[8][8];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rb = 4 * wave + (lane >> 4);  // row block (8 rows)
+  const int cb = lane & 15;               // column block (16 columns)
+  const int r0 = 8 * rb, c0 = 16 * cb;
+  f2 A[8][8];  // A[r][j] = columns c0 + 2j, c0 + 2j + 1 of row r0 + r
 #pragma unroll
   for (int r = 0; r < 8; ++r)
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-      A[r][c] = (r0 + r < n && c0 + c < n) ? G[(int64_t)(r0 + r) * n + c0 + c] : 0.0f;
-
-  // reflector for column k, by the wave that owns it (lanes of block col k>>3)
-  auto reflector = [&](int k) {
-    const int kb = k >> 3, cc = k & 7;
-    if (wave != (kb >> 1)) return;
-    const bool mine = bj == kb;  // my half of the wave holds column k
-    float x[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      float t = 0.0f;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) t = (c == cc) ? A[r][c] : t;
-      x[r] = mine ? t : 0.0f;
+    for (int c = 0; c < 16; c += 4) {
+      float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r0 + r < n && c0 + c < n) g = *reinterpret_cast<const float4*>(G + (int64_t)(r0 + r) * n + c0 + c);
+      A[r][c / 2] = f2{g.x, g.y};
+      A[r][c / 2 + 1] = f2{g.z, g.w};
     }
+
+  // reflector for column k (= row k), by the 16-lane group holding row k;
+  // the row inside the 8 x 16 block, k & 7, is a compile-time constant RR
+  // (the step loop is unrolled by 8) so A stays in registers
+  auto reflector = [&](int k, auto rr_c) {
+    constexpr int RR = decltype(rr_c)::value;
+    if (wave != (k >> 5)) return;  // wave-uniform
+    const bool mine = rb == (k >> 3);
     float s = 0.0f, x0 = 0.0f, dkk = 0.0f;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int i = r0 + r;
-      if (i >= k + 2) s += x[r] * x[r];
-      if (i == k + 1) x0 = x[r];
-      if (i == k) dkk = x[r];
+    for (int c = 0; c < 16; ++c) {
+      const int j = c0 + c;
+      const float x = A[RR][c >> 1][c & 1];
+      if (j >= k + 2) s += x * x;
+      if (j == k + 1) x0 = x;
+      if (j == k) dkk = x;
     }
-    s = wave_sum_dpp(s);
-    x0 = wave_sum_dpp(x0);
-    dkk = wave_sum_dpp(dkk);
+    s = row16_sum(s);
+    x0 = row16_sum(x0);
+    dkk = row16_sum(dkk);
     float tau = 0.0f, beta = x0, scal = 0.0f;
     if (s > 0.0f) {
       const float nrm = sqrtf(x0 * x0 + s);
@@ -112,83 +153,151 @@ __global__ void __launch_bounds__(1024)
       tau = (beta - x0) / beta;
       scal = 1.0f / (x0 - beta);
     }
-    float* v = vs[k & 1];
     if (mine) {
+      float* v = vs[k & 1];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const int i = r0 + r;
-        float vi = 0.0f;
-        if (i == k + 1) vi = 1.0f;
-        else if (i > k + 1) vi = x[r] * scal;
-        v[i] = tau != 0.0f ? vi : 0.0f;
-        if (i > k && i < n) Vh[(int64_t)k * n + i] = vi;
+      for (int c = 0; c < 16; c += 4) {  // 16-B LDS and global stores
+        float4 t, g;
+        float* tp = &t.x;
+        float* gp = &g.x;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = c0 + c + e;
+          float vj = 0.0f;
+          if (j == k + 1) vj = 1.0f;
+          else if (j > k + 1) vj = A[RR][(c + e) >> 1][(c + e) & 1] * scal;
+          gp[e] = vj;  // Vh row k: entries j <= k are never read (form_q masks them)
+          tp[e] = tau != 0.0f ? vj : 0.0f;
+        }
+        *reinterpret_cast<float4*>(v + c0 + c) = t;
+        if (c0 + c < n) *reinterpret_cast<float4*>(Vh + (int64_t)k * n + c0 + c) = g;
       }
-    }
-    if (lane == 0) {
-      tsh[k & 1] = tau;
-      tdiag[k] = dkk;
-      toff[k] = beta;
-      tau_out[k] = tau;
+      if (cb == 0) {
+        tsh[k & 1] = tau;
+        tdiag[k] = dkk;
+        toff[k] = beta;
+        tau_out[k] = tau;
+      }
     }
   };
 
-  if (n > 2) reflector(0);
+  if (n > 2) reflector(0, std::integral_constant<int, 0>{});
   __syncthreads();
-  for (int k = 0; k < n - 2; ++k) {
+  TRI_PROF_DECL
+  auto step = [&](int k, auto rr_next) {
+    constexpr int RN = decltype(rr_next)::value;  // row of reflector k+1 in its block
+    TRI_PROF_MARK(0)
     const float tau = tsh[k & 1];
     const float* v = vs[k & 1];
-    if (tau != 0.0f) {
-      // p partials over my 8 columns; v^T (A v) partial for K
-      float vc[8];
+    const bool active = 32 * wave + 31 >= k + 1;  // wave-uniform: rows > k present
+    const bool owner = wave == ((k + 1) >> 5);    // forms reflector k+1 inside its update
+    f2 vc[8];
+    if (tau != 0.0f && active) {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) vc[c] = v[c0 + c];
-      float vav = 0.0f;
+      for (int c = 0; c < 16; c += 4) {
+        const float4 t = *reinterpret_cast<const float4*>(v + c0 + c);
+        vc[c / 2] = f2{t.x, t.y};
+        vc[c / 2 + 1] = f2{t.z, t.w};
+      }
+      // row partials of A v over my 16 columns
+      float pr[8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        float acc = 0.0f;
+        f2 acc = A[r][0] * vc[0];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) acc += A[r][c] * vc[c];
-        part[bj * 257 + r0 + r] = acc;
-        vav += v[r0 + r] * acc;
+        for (int j = 1; j < 8; ++j) acc = A[r][j] * vc[j] + acc;
+        pr[r] = acc.x + acc.y;
       }
-      vav = wave_sum_dpp(vav);
-      if (lane == 0) red[k & 1][wave] = vav;
-      __syncthreads();
-      if (tid < 256) {
-        float acc = 0.0f;
-#pragma unroll 8
-        for (int j = 0; j < 32; ++j) acc += part[j * 257 + tid];
-        ps[tid] = tau * acc;
+      // reduce-scatter of the 8 row sums over the 16 lanes
+      const int b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1, b1 = (lane >> 1) & 1;
+      float q4[4], q2[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float keep = b3 ? pr[4 + i] : pr[i];
+        const float send = b3 ? pr[i] : pr[4 + i];
+        q4[i] = keep + dpp<DPP_ROR8>(send);
       }
-      float vAv = 0.0f;
 #pragma unroll
-      for (int w = 0; w < 16; ++w) vAv += red[k & 1][w];
-      const float K = 0.5f * tau * tau * vAv;
-      __syncthreads();
-      // A -= v w^T + w v^T
-      float wc[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) wc[c] = ps[c0 + c] - K * vc[c];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const float vr = v[r0 + r];
-        const float wr = ps[r0 + r] - K * vr;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) A[r][c] -= vr * wc[c] + wr * vc[c];
+      for (int i = 0; i < 2; ++i) {
+        const float keep = b2 ? q4[2 + i] : q4[i];
+        const float send = b2 ? q4[i] : q4[2 + i];
+        q2[i] = keep + dpp<DPP_HALF_MIRROR>(send);
       }
+      float q1 = (b1 ? q2[1] : q2[0]) + dpp<DPP_XOR2>(b1 ? q2[0] : q2[1]);
+      q1 += dpp<DPP_XOR1>(q1);
+      if ((lane & 1) == 0) ps[r0 + 4 * b3 + 2 * b2 + b1] = tau * q1;
     }
-    if (k + 1 < n - 2) reflector(k + 1);
-    __syncthreads();
+    TRI_PROF_MARK(1)
+    lds_barrier();
+    TRI_PROF_MARK(2)
+    bool reflected = false;
+    if (tau != 0.0f && active) {
+      // K = (tau / 2) v.p over the whole vector, by every wave
+      const float4 pv = *reinterpret_cast<const float4*>(ps + 4 * lane);
+      const float4 vv = *reinterpret_cast<const float4*>(v + 4 * lane);
+      const float K = 0.5f * tau * wave_sum_dpp(pv.x * vv.x + pv.y * vv.y + pv.z * vv.z + pv.w * vv.w);
+      const f2 K2 = f2{K, K};
+      f2 wc[8];
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) {
+        const float4 t = *reinterpret_cast<const float4*>(ps + c0 + c);
+        wc[c / 2] = f2{t.x, t.y} - K2 * vc[c / 2];
+        wc[c / 2 + 1] = f2{t.z, t.w} - K2 * vc[c / 2 + 1];
+      }
+      float vr[8], wr[8];
+#pragma unroll
+      for (int r = 0; r < 8; r += 4) {
+        const float4 a4 = *reinterpret_cast<const float4*>(v + r0 + r);
+        const float4 b4 = *reinterpret_cast<const float4*>(ps + r0 + r);
+        vr[r] = a4.x, vr[r + 1] = a4.y, vr[r + 2] = a4.z, vr[r + 3] = a4.w;
+        wr[r] = b4.x - K * a4.x, wr[r + 1] = b4.y - K * a4.y;
+        wr[r + 2] = b4.z - K * a4.z, wr[r + 3] = b4.w - K * a4.w;
+      }
+      // A -= v w^T + w v^T, two packed FMAs per column pair; row RN first,
+      // so the owner forms reflector k+1 before the other 7 rows
+      auto upd = [&](int r) {
+        const f2 nv = f2{-vr[r], -vr[r]}, nw = f2{-wr[r], -wr[r]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) A[r][j] = nw * vc[j] + (nv * wc[j] + A[r][j]);
+      };
+      upd(RN);
+      if (owner && k + 1 < n - 2) {
+        __builtin_amdgcn_s_setprio(2);
+        reflector(k + 1, rr_next);
+        __builtin_amdgcn_s_setprio(0);
+        reflected = true;
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (r != RN) upd(r);
+    }
+    TRI_PROF_MARK(3)
+    if (!reflected && k + 1 < n - 2) reflector(k + 1, rr_next);  // tau == 0 step
+    TRI_PROF_MARK(4)
+    lds_barrier();
+    TRI_PROF_MARK(5)
+  };
+  for (int kb = 0; kb < n - 2; kb += 8) {
+    step(kb + 0, std::integral_constant<int, 1>{});
+    if (kb + 1 < n - 2) step(kb + 1, std::integral_constant<int, 2>{});
+    if (kb + 2 < n - 2) step(kb + 2, std::integral_constant<int, 3>{});
+    if (kb + 3 < n - 2) step(kb + 3, std::integral_constant<int, 4>{});
+    if (kb + 4 < n - 2) step(kb + 4, std::integral_constant<int, 5>{});
+    if (kb + 5 < n - 2) step(kb + 5, std::integral_constant<int, 6>{});
+    if (kb + 6 < n - 2) step(kb + 6, std::integral_constant<int, 7>{});
+    if (kb + 7 < n - 2) step(kb + 7, std::integral_constant<int, 0>{});
   }
+  TRI_PROF_FLUSH
   // the last 2 x 2 block
 #pragma unroll
   for (int r = 0; r < 8; ++r)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < 16; ++c) {
       const int i = r0 + r, j = c0 + c;
-      if (i == n - 2 && j == n - 2) tdiag[n - 2] = A[r][c];
-      if (i == n - 1 && j == n - 1) tdiag[n - 1] = A[r][c];
-      if (i == n - 1 && j == n - 2) toff[n - 2] = A[r][c];
+      const float x = A[r][c >> 1][c & 1];
+      if (i == n - 2 && j == n - 2) tdiag[n - 2] = x;
+      if (i == n - 1 && j == n - 1) tdiag[n - 1] = x;
+      if (i == n - 1 && j == n - 2) toff[n - 2] = x;
     }
   if (tid == 0) {
     toff[n - 1] = 0.0f;
@@ -197,41 +306,50 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
-// One wave per column c of Q: q = H_0 (H_1 (... H_{n-3} e_c)); H_k leaves
-// columns c <= k alone, so the product starts at k = min(c-1, n-3).
+// Q = H_0 H_1 ... H_{n-3}: one wave per column c of Q, q = H_0 (H_1 (...
+// H_{n-3} e_c)); H_k leaves columns c <= k alone, so the product starts at
+// k = min(c-1, n-3).  The reflectors are staged through LDS FQ_KB at a time
+// by all 8 waves of the workgroup (one coalesced load per block instead of a
+// dependent L2 round trip per reflector), then applied from LDS.
 // RPL = rows per lane (n <= 64 * RPL).
+constexpr int FQ_KB = 16;
 template <int RPL>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(512)
     form_q_kernel(const float* __restrict__ Vh, const float* __restrict__ tau, int n, float* Q) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (c >= n) return;  // no barriers below
+  __shared__ __attribute__((aligned(16))) float vsh[FQ_KB][64 * RPL];
+  __shared__ float tsh[FQ_KB];
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 8 + (threadIdx.x >> 6);
+  const int c_first = blockIdx.x * 8;
   float q[RPL];
 #pragma unroll
   for (int r = 0; r < RPL; ++r) q[r] = (lane + 64 * r == c) ? 1.0f : 0.0f;
-  int k = c - 1 < n - 3 ? c - 1 : n - 3;
-  float vn[RPL];
-  auto load = [&](int kk, float* dst) {
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) {
-      const int row = lane + 64 * r;
-      dst[r] = (kk >= 0 && row > kk && row < n) ? Vh[(int64_t)kk * n + row] : 0.0f;
+  const int kstart = c < n ? (c - 1 < n - 3 ? c - 1 : n - 3) : -1;
+  // highest reflector any column of this workgroup needs
+  int ktop = c_first + 7 - 1 < n - 3 ? c_first + 7 - 1 : n - 3;
+  if (ktop >= n) ktop = n - 1;
+  for (int kb = ktop - (ktop % FQ_KB); kb >= 0; kb -= FQ_KB) {
+    __syncthreads();  // previous block consumed
+    for (int s = threadIdx.x; s < FQ_KB * 64 * RPL; s += 512) {
+      const int kk = kb + s / (64 * RPL), row = s % (64 * RPL);
+      vsh[s / (64 * RPL)][row] = (kk <= ktop && row > kk && row < n) ? Vh[(int64_t)kk * n + row] : 0.0f;
     }
-  };
-  load(k, vn);
-  for (; k >= 0; --k) {
-    float vk[RPL];
+    if (threadIdx.x < FQ_KB) tsh[threadIdx.x] = kb + (int)threadIdx.x <= ktop ? tau[kb + threadIdx.x] : 0.0f;
+    __syncthreads();
+    for (int j = FQ_KB - 1; j >= 0; --j) {
+      const int k = kb + j;
+      if (k > kstart) continue;  // wave-uniform
+      const float t = tsh[j];
+      if (t == 0.0f) continue;
+      float d = 0.0f;
 #pragma unroll
-    for (int r = 0; r < RPL; ++r) vk[r] = vn[r];
-    const float t = tau[k];
-    load(k - 1, vn);  // prefetch the next reflector under this one's reduction
-    if (t == 0.0f) continue;
-    float d = 0.0f;
+      for (int r = 0; r < RPL; ++r) d += vsh[j][lane + 64 * r] * q[r];
+      d = wave_sum_dpp(d) * t;
 #pragma unroll
-    for (int r = 0; r < RPL; ++r) d += vk[r] * q[r];
-    d = wave_sum(d) * t;
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) q[r] -= d * vk[r];
+      for (int r = 0; r < RPL; ++r) q[r] -= d * vsh[j][lane + 64 * r];
+    }
   }
+  if (c >= n) return;
 #pragma unroll
   for (int r = 0; r < RPL; ++r) {
     const int row = lane + 64 * r;
@@ -337,19 +455,19 @@ hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, flo
                           float* tau, hipStream_t s, float* work) {
   if (wide_dim(Dp)) return launch_wide_tridiag(G, Dp, tdiag, toff, Vh, tau, work, s);
   if (Dp < 4 || Dp > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(1024), 0, s, G, Dp, tdiag, toff, Vh, tau);
+  hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(512), 0, s, G, Dp, tdiag, toff, Vh, tau);
   return hipGetLastError();
 }
 
 hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s) {
   if (Dp < 4 || Dp > 1024) return hipErrorInvalidValue;
-  const dim3 grid((unsigned)((Dp + 3) / 4));
+  const dim3 grid((unsigned)((Dp + 7) / 8));
   if (Dp <= 256)
-    hipLaunchKernelGGL(form_q_kernel<4>, grid, dim3(256), 0, s, Vh, tau, Dp, Q);
+    hipLaunchKernelGGL(form_q_kernel<4>, grid, dim3(512), 0, s, Vh, tau, Dp, Q);
   else if (Dp <= 512)
-    hipLaunchKernelGGL(form_q_kernel<8>, grid, dim3(256), 0, s, Vh, tau, Dp, Q);
+    hipLaunchKernelGGL(form_q_kernel<8>, grid, dim3(512), 0, s, Vh, tau, Dp, Q);
   else
-    hipLaunchKernelGGL(form_q_kernel<16>, grid, dim3(256), 0, s, Vh, tau, Dp, Q);
+    hipLaunchKernelGGL(form_q_kernel<16>, grid, dim3(512), 0, s, Vh, tau, Dp, Q);
   return hipGetLastError();
 }
 
