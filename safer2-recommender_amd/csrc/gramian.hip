@@ -126,19 +126,56 @@ __global__ void __launch_bounds__(GramCfg<T>::NTHR)
   }
 }
 
+// Sum of the nblk partial slabs, four consecutive elements (one float4) of
+// the lower tiles per thread.  The blocks are cut into kRedChains contiguous
+// ranges summed as independent chains (many loads in flight per thread: the
+// read is bandwidth-, not latency-bound), then combined in chain order -- a
+// fixed order, so the result is deterministic.  Then mirrored into G.
+constexpr int kRedChains = 8;
 template <int T>
 __global__ void __launch_bounds__(256)
     gram_reduce_kernel(const float* __restrict__ P, int64_t nblk, float* __restrict__ G) {
   constexpr int Dp = 32 * T, NT = T * (T + 1) / 2;
-  const int el = blockIdx.x * 256 + threadIdx.x;
-  if (el >= Dp * Dp) return;
-  const int gi = el / Dp, gj = el % Dp;
-  if (gi < gj) return;
-  const int64_t off = tidx(gi >> 5, gj >> 5) * 1024 + (gi & 31) * 32 + (gj & 31);
-  float s = 0.0f;
-  for (int64_t b = 0; b < nblk; ++b) s += P[b * NT * 1024 + off];
-  G[gi * Dp + gj] = s;
-  G[gj * Dp + gi] = s;
+  const int q = blockIdx.x * 256 + threadIdx.x;  // float4 index within a slab
+  if (q >= NT * 256) return;
+  const int64_t stride = (int64_t)NT * 1024;
+  float4 acc[kRedChains];
+  const int64_t per = (nblk + kRedChains - 1) / kRedChains;
+#pragma unroll
+  for (int c = 0; c < kRedChains; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = 0; i < per; ++i) {
+#pragma unroll
+    for (int c = 0; c < kRedChains; ++c) {
+      const int64_t b = c * per + i;
+      if (b < nblk) {
+        const float4 v = reinterpret_cast<const float4*>(P + b * stride)[q];
+        acc[c].x += v.x;
+        acc[c].y += v.y;
+        acc[c].z += v.z;
+        acc[c].w += v.w;
+      }
+    }
+  }
+  float4 s = acc[0];
+#pragma unroll
+  for (int c = 1; c < kRedChains; ++c) {
+    s.x += acc[c].x;
+    s.y += acc[c].y;
+    s.z += acc[c].z;
+    s.w += acc[c].w;
+  }
+  const int t = q >> 8, e0 = (q & 255) * 4;  // tile, first element (row-major 32 x 32)
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= t) ++I;
+  const int J = t - I * (I + 1) / 2;
+  const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int gi = 32 * I + ((e0 + u) >> 5), gj = 32 * J + ((e0 + u) & 31);
+    if (gi < gj) continue;  // diagonal tiles: the lower half only
+    G[gi * Dp + gj] = sv[u];
+    G[gj * Dp + gi] = sv[u];
+  }
 }
 
 // Dp = 8, 16: thread (i, j) of one Dp x Dp partial per workgroup.
@@ -182,7 +219,8 @@ hipError_t launch_tiled(const GramArgs& a, hipStream_t s) {
                        a, rpb);
   else
     return hipMemsetAsync(a.G, 0, sizeof(float) * Dp * Dp, s);
-  hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3((Dp * Dp + 255) / 256), dim3(256), 0, s,
+  constexpr int NT = T * (T + 1) / 2;
+  hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3((NT * 256 + 255) / 256), dim3(256), 0, s,
                      a.partials, nblk, a.G);
   return hipGetLastError();
 }
