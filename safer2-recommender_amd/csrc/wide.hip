@@ -6,13 +6,13 @@
 // erm_mf.h:91-210, cvar_mf.h:182-229) is split across kernels with A in an
 // HBM workspace, a bounded batch of entities at a time:
 //
-//   wide_syrk_kernel<1>  grid (entity, 128x128 block pair of A's lower
-//                        triangle): the pair's 16 32x32 tiles accumulate
-//                        X_h^T D X_h over the gathered history rows with
-//                        v_mfma_f32_32x32x2_f32 (rows staged through LDS, 16
-//                        per chunk, one chunk ahead; row ids two chunks
-//                        ahead), starting from the G part of A; the diagonal
-//                        pairs also form their 128 entries of b.
+//   wide_syrk2_kernel<1> grid (entity, 256x256 block pair of A's lower
+//                        triangle): the pair's 32x32 tiles accumulate
+//                        X_h^T D X_h over the gathered history rows as
+//                        split-bf16 MFMAs (fp32-accurate; rows staged through
+//                        LDS as bf16 pieces, 16 per chunk, one chunk ahead),
+//                        two-level accumulation, the G part of A added in the
+//                        epilogue; the diagonal pairs also form b.
 //   wide_chol_kernel     one workgroup (8 waves) per entity: right-looking
 //                        blocked Cholesky over the workspace tiles -- the
 //                        diagonal tile factored and inverted in LDS
@@ -34,7 +34,7 @@
 //   rot_wide_kernel      Y = X Q / X Q^T, 64 rows x 128 columns per
 //                        workgroup, K streamed in 32-wide slabs; also the
 //                        u^T G u partials of the user loss.
-// and the Gramian: wide_syrk_kernel<0> (split-K over row blocks x block
+// and the Gramian: wide_syrk2_kernel<0> (split-K over row blocks x block
 // pairs) + wide_gram_reduce_kernel (fixed order, deterministic).
 #include <hip/hip_runtime.h>
 
@@ -50,8 +50,6 @@ namespace {
 
 constexpr int WB = 128;    // block-pair edge
 constexpr int WR = 16;     // rows per staged chunk
-constexpr int WRING = 4;   // row-id ring slots
-constexpr int WFLUSH = 256; // chunks (x WR rows) per accumulator flush
 constexpr int kWideMaxBlocks = 64;
 
 __device__ __forceinline__ void pair_of(int pidx, int& BI, int& BJ) {
@@ -88,25 +86,59 @@ __device__ __forceinline__ bool xcd_unit(int P, int64_t n_units, int64_t& unit, 
   return unit < n_units;
 }
 
-// MODE 0: partial Gramian of the unit's rows [r0, r1) (operand weight g.w);
-// MODE 1: assembly of entity order[pos0 + unit] into its workspace slot.
+// ---- SYRK of A (MODE 1) / partial Gramians (MODE 0) over 256 x 256 block
+// pairs, fp32 products on the bf16 matrix cores ----
+// One workgroup per (unit, block pair of A's lower triangle): MODE 1 unit =
+// entity (the pair's tiles of X_h^T D X_h from the gathered history rows,
+// plus the G part of A and its b in the epilogue), MODE 0 unit = row block
+// of the Gramian.  Products as common.h mfma_x6 (3-piece bf16 splits,
+// fp32-accurate).  A pair of 256-column blocks per workgroup: every gathered
+// row is read 2x per entity at Dp = 512 (3 pairs), 4x at Dp = 1024 (10
+// pairs) -- half the re-reads of 128-wide pairs.  512 threads:
+//  * staging: one thread per staged column (512 for an off-diagonal pair:
+//    block BI then block BJ; 256 x two row halves for a diagonal one) gathers
+//    its 16 (8) rows of the chunk, scales them (sqrt(nu) for the V kinds,
+//    the row weight on the B side of a weighted Gramian), splits them into
+//    3 bf16 pieces and writes the k-major granules the MFMA lanes read
+//    (granule (piece p, row half hh, column c) = rows 8hh..8hh+7 of c);
+//  * MFMAs: wave w owns tile row w of an off-diagonal pair (8 tiles, its A
+//    fragments shared), or tiles w, w+8, ... of a diagonal pair's 36.
+// Chunks of 16 rows (one k16 step), double-buffered; the next chunk's rows
+// are loaded one iteration ahead, row ids three ahead.  Two-level
+// accumulation as wide_syrk_kernel (flush into the unit's output tiles
+// every W2FLUSH chunks).
+constexpr int WB2 = 256;
+constexpr int W2R = 16;
+constexpr int W2RING = 4;
+constexpr int W2FLUSH = 128;
+constexpr int W2GRAN = 6 * 512;  // 16-B granules per stage buffer
+
+__device__ __forceinline__ int g2(int p, int hh, int c) { return (p * 2 + hh) * 512 + c; }
+
+int wide_pairs2(int Dp) {
+  const int nb = Dp / WB2;
+  return nb * (nb + 1) / 2;
+}
+
 template <int MODE>
-__global__ void __launch_bounds__(256, 3)  // 3 waves per SIMD (<= 168 registers)
-    wide_syrk_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws,
-                     int64_t n_units) {
-  __shared__ __attribute__((aligned(16))) float xa[2][WR * WB];
-  __shared__ __attribute__((aligned(16))) float xb[2][WR * WB];
-  __shared__ int ring_id[WRING * WR];
-  __shared__ float ring_sa[WRING * WR], ring_bw[WRING * WR];
+__global__ void __launch_bounds__(512)
+    wide_syrk2_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws,
+                      int64_t n_units) {
+  __shared__ __attribute__((aligned(16))) bf16x8 stage[2][W2GRAN];
+  __shared__ int ring_id[W2RING * W2R];
+  __shared__ float ring_sa[W2RING * W2R], ring_bw[W2RING * W2R];
+  __shared__ float bred[WB2];
   const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int T = Dp >> 5, NT = T * (T + 1) / 2, NB = Dp / WB;
+  const int T = Dp >> 5, NT = T * (T + 1) / 2, NB = Dp / WB2;
   int64_t unit;
   int pidx;
   if (!xcd_unit(NB * (NB + 1) / 2, n_units, unit, pidx)) return;
   int BI, BJ;
   pair_of(pidx, BI, BJ);
   const bool dgp = BI == BJ;
+  // a diagonal pair stages one block (A = B) unless its B side is weighted
+  const bool same = dgp && !(MODE == 0 && g.w != nullptr);
   const int kind = a.kind;
   const bool vk = MODE == 1 && is_v_kind(kind);
 
@@ -121,15 +153,15 @@ __global__ void __launch_bounds__(256, 3)  // 3 waves per SIMD (<= 168 registers
     e = rec.entity;
     h = rec.h;
     p0 = rec.p0;
-    if (h == 0) return;  // untouched entity (no workgroup barrier passed yet)
+    if (h == 0) return;  // untouched entity (no barrier passed yet)
     int64_t extra = 0;
     if (vk && a.quirk && h > 128 && (h % 128) != 0) extra = 128 - (h % 128);
     nrow = h + extra;
   }
-  const int nchunks = (int)((nrow + WR - 1) / WR);
+  const int nchunks = (int)((nrow + W2R - 1) / W2R);
 
   auto ring_load = [&](int c, int& id, float& sa, float& bw) {
-    const int64_t k = (int64_t)c * WR + tid;
+    const int64_t k = (int64_t)c * W2R + tid;
     id = -1;
     sa = 0.0f;
     bw = 0.0f;
@@ -152,218 +184,215 @@ __global__ void __launch_bounds__(256, 3)  // 3 waves per SIMD (<= 168 registers
     }
   };
   auto ring_store = [&](int c, int id, float sa, float bw) {
-    const int s = (c % WRING) * WR + tid;
-    ring_id[s] = id;
-    ring_sa[s] = sa;
-    ring_bw[s] = bw;
+    const int sl = (c % W2RING) * W2R + tid;
+    ring_id[sl] = id;
+    ring_sa[sl] = sa;
+    ring_bw[sl] = bw;
   };
   const float* X = MODE == 0 ? g.X : a.X;
-  float4 regs[4];
-  auto load_data = [&](int c) {
-    const int slot = c % WRING;
+  // staging role: column sc of the staged image, rows 8*hh0 .. 8*hh0 + 8*nh - 1
+  const int sc = same ? (tid & (WB2 - 1)) : tid;
+  const int hh0 = same ? (tid >> 8) : 0;
+  const int xcol = sc < WB2 ? WB2 * BI + sc : WB2 * BJ + (sc - WB2);
+  const bool wside = MODE == 0 && !same && sc >= WB2;  // weighted B operand
+  const bool bown = MODE == 1 && dgp;                  // diagonal pairs form b
+  float xr[16];
+  auto load = [&](int c) {
+    const int base = (c % W2RING) * W2R + 8 * hh0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int sidx = tid + 256 * q;
-      const int r = sidx >> 6, f = sidx & 63;
-      regs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!(dgp && f >= 32)) {
-        const int col = f < 32 ? WB * BI + 4 * f : WB * BJ + 4 * (f - 32);
-        const int id = ring_id[slot * WR + r];
-        if (id >= 0) regs[q] = *reinterpret_cast<const float4*>(X + (int64_t)id * Dp + col);
-      }
+    for (int r = 0; r < 16; ++r) {
+      if (same && r >= 8) break;
+      const int id = ring_id[base + r];
+      // no select on the loaded value (rows past the end have sa = 0): the
+      // loads stay in flight through the MFMAs of the current chunk
+      xr[r] = X[(int64_t)max(id, 0) * Dp + xcol];
     }
   };
-  auto store_stage = [&](int buf, int c) {
-    const int slot = c % WRING;
+  float bpart = 0.0f, btot = 0.0f;
+  auto stage_write = [&](int buf, int c) {
+    const int base = (c % W2RING) * W2R + 8 * hh0;
+    bf16x8* st = stage[buf];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int sidx = tid + 256 * q;
-      const int r = sidx >> 6, f = sidx & 63;
-      if (dgp && f >= 32) continue;
-      float4 v = regs[q];
-      const float sa = ring_sa[slot * WR + r];
-      if (MODE == 1 && vk) {
-        v.x *= sa;
-        v.y *= sa;
-        v.z *= sa;
-        v.w *= sa;
+    for (int hh = 0; hh < 2; ++hh) {
+      if (same && hh > 0) break;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = 8 * hh + j;
+        const float sa = ring_sa[base + r];
+        float x = xr[r] * sa;
+        if (bown) bpart += ring_bw[base + r] * x;
+        if (wside) x *= ring_bw[base + r];
+        v[j] = x;
       }
-      float4 vb = v;
-      if (MODE == 0) {  // B operand carries the row weight
-        const float bw = ring_bw[slot * WR + r];
-        vb.x *= bw;
-        vb.y *= bw;
-        vb.z *= bw;
-        vb.w *= bw;
-      }
-      if (f < 32) {
-        *reinterpret_cast<float4*>(&xa[buf][r * WB + 4 * f]) = v;
-        if (dgp) *reinterpret_cast<float4*>(&xb[buf][r * WB + 4 * f]) = vb;
-      } else {
-        *reinterpret_cast<float4*>(&xb[buf][r * WB + 4 * (f - 32)]) = vb;
-      }
+      bf16x8 f[3];
+      split3x8(v, f);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) st[g2(p, hh0 + hh, sc)] = f[p];
     }
   };
 
-  if (tid < WR && nchunks > 0) {
-    int id;
-    float sa, bw;
-    ring_load(0, id, sa, bw);
-    ring_store(0, id, sa, bw);
-    if (nchunks > 1) {
-      ring_load(1, id, sa, bw);
-      ring_store(1, id, sa, bw);
-    }
-  }
+  // tiles of this wave (block-local 32x32 tile coordinates): tile row I, all
+  // 8 tile columns J (J <= I on a diagonal pair).  I = w for waves 0..3 and
+  // 11 - w for 4..7, so the two waves of a SIMD (w, w + 4) hold rows
+  // summing to 7: 9 tiles per SIMD on a diagonal pair, 16 on the others.
+  constexpr int MT = 8;
+  const int tI = wave < 4 ? wave : 11 - wave;
+  auto tv = [&](int m) { return !dgp || m <= tI; };  // wave-uniform
+  const int boff = same ? 0 : WB2;  // B operand columns in the staged image
 
-  // accumulators start from the G part of A (MODE 1, as solve.hip):
-  //  iALS w*G + lam*I, U h*w*G, V w*G, CVaR 0
-  const float hf = (float)h;
-  float omega = 1.0f, lam = 0.0f;
-  const bool grad = MODE == 1 && is_grad_kind(kind);
-  if (MODE == 1) {
-    omega = (is_u_kind(kind) && a.entity_weight) ? a.entity_weight[e] : 1.0f;
-    lam = entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other, a.entity_reg, e,
-                        a.lambda_is_reg);
-  }
-  const float gscale = kind == KIND_IALS ? a.w : (is_u_kind(kind) ? hf * a.w : a.w);
-  // Two-level accumulation: the MFMAs accumulate at most WFLUSH chunks of
-  // rows from zero, then the chunk sum is added into the unit's own output
-  // tiles (workspace slot / Gramian partial; this workgroup is their only
-  // writer, so no atomics).  One MFMA accumulator over a ~190K-row history
-  // (MSD head items) drifts by ~2e-4 relative; chunk sums keep the error at
-  // the level of a WFLUSH * WR-row sum.  The G part of A joins in the epilogue.
   float* const otile0 = MODE == 0 ? g.partials + unit * NT * 1024
                                   : ws + unit * ((int64_t)NT * 1024 + Dp);
-  auto otile = [&](int j) {
-    return otile0 + (int64_t)tidx(4 * BI + wave, 4 * BJ + j) * 1024;
-  };
+  auto otile = [&](int m) { return otile0 + (int64_t)tidx(8 * BI + tI, 8 * BJ + m) * 1024; };
   bool flushed = false;
-  f32x16 acc[4];
+  f32x16 acc[MT];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = f32x16{0.f};
-  float bacc = 0.0f, btot = 0.0f;
+  for (int m = 0; m < MT; ++m) acc[m] = f32x16{0.f};
   auto flush = [&]() {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!dgp || j <= wave) {  // wave-uniform
-        float* t = otile(j);
+    for (int m = 0; m < MT; ++m) {
+      if (tv(m)) {  // wave-uniform
+        float* t = otile(m);
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          float* p = t + acc_row(q, hi) * 32 + lo;
-          *p = flushed ? *p + acc[j][q] : acc[j][q];
+          float* pq = t + acc_row(q, hi) * 32 + lo;
+          *pq = flushed ? *pq + acc[m][q] : acc[m][q];
         }
       }
-      acc[j] = f32x16{0.f};
-      __builtin_amdgcn_sched_barrier(0);  // one tile's 16 values live at a time
+      acc[m] = f32x16{0.f};
+      __builtin_amdgcn_sched_barrier(0);
     }
-    btot += bacc;
-    bacc = 0.0f;
+    btot += bpart;
+    bpart = 0.0f;
     flushed = true;
   };
+
+  if (tid < W2R) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      if (c < nchunks) {
+        int id;
+        float sa, bw;
+        ring_load(c, id, sa, bw);
+        ring_store(c, id, sa, bw);
+      }
+  }
   lds_barrier();
   if (nchunks > 0) {
-    load_data(0);
-    store_stage(0, 0);
+    load(0);
+    stage_write(0, 0);
   }
+  if (nchunks > 1) load(1);
   lds_barrier();
 
   for (int c = 0; c < nchunks; ++c) {
     const int buf = c & 1;
     const bool more = c + 1 < nchunks;
-    const bool ring_more = (tid < WR) && (c + 2 < nchunks);
-    if (more) load_data(c + 1);
+    const bool ring_more = (tid < W2R) && (c + 3 < nchunks);
     int nid = -1;
     float nsa = 0.f, nbw = 0.f;
-    if (ring_more) ring_load(c + 2, nid, nsa, nbw);
-    const float* sa_ = xa[buf];
-    const float* sb_ = xb[buf];
+    if (ring_more) ring_load(c + 3, nid, nsa, nbw);
+    const bf16x8* st = stage[buf];
+    {
+      // A fragments of the wave's tile row, shared by its tiles; B fragments
+      // one tile ahead of their MFMAs (a deeper hoist of the LDS reads would
+      // not fit the 256 registers next to 8 accumulators)
+      bf16x8 af[3], bcur[3], bnxt[3];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!dgp || j <= wave) {  // wave-uniform
+      for (int p = 0; p < 3; ++p) {
+        af[p] = st[g2(p, hi, 32 * tI + lo)];
+        bcur[p] = st[g2(p, hi, boff + lo)];
+      }
 #pragma unroll
-        for (int s = 0; s < WR / 2; ++s) {
-          const int row = 2 * s + hi;
-          acc[j] = mfma32(sa_[row * WB + 32 * wave + lo], sb_[row * WB + 32 * j + lo], acc[j]);
+      for (int m = 0; m < MT; ++m) {
+        if (tv(m)) {
+          if (m + 1 < MT) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bnxt[p] = st[g2(p, hi, boff + 32 * (m + 1) + lo)];
+          }
+          acc[m] = mfma_x6(af, bcur, acc[m]);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) bcur[p] = bnxt[p];
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (MODE == 1 && dgp && tid < WB) {
-      const int slot = c % WRING;
-#pragma unroll 4
-      for (int r = 0; r < WR; ++r) bacc += ring_bw[slot * WR + r] * sa_[r * WB + tid];
+    if ((c + 1) % W2FLUSH == 0 && more) flush();  // block-uniform
+    if (more) {
+      stage_write(buf ^ 1, c + 1);  // chunk c+1's rows (loaded last iteration)
+      if (c + 2 < nchunks) load(c + 2);
     }
-    if ((c + 1) % WFLUSH == 0 && more) flush();  // block-uniform
-    if (more) store_stage(buf ^ 1, c + 1);
-    if (ring_more) ring_store(c + 2, nid, nsa, nbw);
+    if (ring_more) ring_store(c + 3, nid, nsa, nbw);
     lds_barrier();
   }
-  if (flushed) {  // fold the stored chunk sums back in (same thread wrote them)
+  if (flushed) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!dgp || j <= wave) {
-        const float* t = otile(j);
+    for (int m = 0; m < MT; ++m) {
+      if (tv(m)) {
+        const float* t = otile(m);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) acc[j][q] += t[acc_row(q, hi) * 32 + lo];
+        for (int q = 0; q < 16; ++q) acc[m][q] += t[acc_row(q, hi) * 32 + lo];
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  bacc += btot;
-  if (MODE == 1 && !grad) {  // G part of A (as solve.hip): iALS w*G + lam*I, U h*w*G, V w*G
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!dgp || j <= wave) {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int gi = WB * BI + 32 * wave + acc_row(q, hi), gj = WB * BJ + 32 * j + lo;
-          float v = gscale * a.G[(int64_t)gi * Dp + gj];
-          if (kind == KIND_IALS && gi == gj) v += lam;
-          acc[j][q] += v;
-        }
-      }
-    }
-  }
+  bpart += btot;
 
   if (MODE == 0) {
-    float* P = g.partials + unit * NT * 1024;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!dgp || j <= wave) {
-        const int I = 4 * BI + wave, J = 4 * BJ + j;
-        float* tile = P + (int64_t)tidx(I, J) * 1024;
+    for (int m = 0; m < MT; ++m) {
+      if (tv(m)) {
+        float* t = otile(m);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) tile[acc_row(q, hi) * 32 + lo] = acc[j][q];
+        for (int q = 0; q < 16; ++q) t[acc_row(q, hi) * 32 + lo] = acc[m][q];
       }
+      __builtin_amdgcn_sched_barrier(0);
     }
     return;
   }
 
-  // epilogue: finish A (per kind, as solve.hip) into the workspace tiles
-  float* slot = ws + unit * ((int64_t)NT * 1024 + Dp);
+  // epilogue: the G part and the per-kind finish of A (as solve.hip)
+  const float hf = (float)h;
+  const float omega = (is_u_kind(kind) && a.entity_weight) ? a.entity_weight[e] : 1.0f;
+  const float lam = entity_lambda(kind, a.reg, a.reg_exp, a.w, a.alpha, h, a.n_other,
+                                  a.entity_reg, e, a.lambda_is_reg);
+  const bool grad = is_grad_kind(kind);
+  const float gscale = kind == KIND_IALS ? a.w : (is_u_kind(kind) ? hf * a.w : a.w);
   const float us = omega / hf;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (!dgp || j <= wave) {
-      const int I = 4 * BI + wave, J = 4 * BJ + j;
-      float* tile = slot + (int64_t)tidx(I, J) * 1024;
+  for (int m = 0; m < MT; ++m) {
+    if (tv(m)) {
+      float* t = otile(m);
+      const int I = 8 * BI + tI, J = 8 * BJ + m;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int i = acc_row(q, hi);
         const int gi = 32 * I + i, gj = 32 * J + lo;
         const bool dg = gi == gj;
-        float v = acc[j][q];
-        if (grad) v = assemble(kind, v, a.G[(int64_t)gi * Dp + gj], dg, a.w, lam, hf, omega);
-        else if (is_u_kind(kind)) v = v * us + (dg ? lam : 0.0f);
-        else if (vk) v = v + (dg ? lam : 0.0f);
-        tile[i * 32 + lo] = v;
+        float v = acc[m][q];
+        const float gv = a.G[(int64_t)gi * Dp + gj];
+        if (grad) {
+          v = assemble(kind, v, gv, dg, a.w, lam, hf, omega);
+        } else {
+          float g0 = gscale * gv;
+          if (kind == KIND_IALS && dg) g0 += lam;
+          v = g0 + v;  // accumulators started from the G part in the fp32 kernels
+          if (is_u_kind(kind)) v = v * us + (dg ? lam : 0.0f);
+          else if (vk) v = v + (dg ? lam : 0.0f);
+        }
+        t[i * 32 + lo] = v;
       }
     }
+    __builtin_amdgcn_sched_barrier(0);  // one tile's G loads live at a time
   }
-  if (dgp && tid < WB) {
-    float b = bacc;
-    if (is_u_kind(kind)) b *= us;  // rhs *= weight / history_size
-    slot[(int64_t)NT * 1024 + WB * BI + tid] = b;
+  if (bown) {  // b of this diagonal block: the two row halves of each column
+    if (tid >= WB2) bred[sc] = bpart;
+    lds_barrier();
+    if (tid < WB2) {
+      float b = bpart + bred[tid];
+      if (is_u_kind(kind)) b *= us;  // rhs *= weight / history_size
+      ws[unit * ((int64_t)NT * 1024 + Dp) + (int64_t)NT * 1024 + WB2 * BI + tid] = b;
+    }
   }
 }
 
@@ -801,11 +830,6 @@ int64_t wide_rows_per_block(int64_t n) {
   return (rpb + WR - 1) / WR * WR;
 }
 
-int wide_pairs(int Dp) {
-  const int nb = Dp / WB;
-  return nb * (nb + 1) / 2;
-}
-
 unsigned xcd_grid(int64_t n_units, int P) { return (unsigned)(((n_units + 7) / 8) * 8 * P); }
 
 size_t wide_chol_lds_bytes(int Dp) {
@@ -833,8 +857,8 @@ hipError_t launch_wide_gramian(int Dp, const GramArgs& g, hipStream_t s) {
   const int64_t nblk = (g.n + rpb - 1) / rpb;
   if (nblk == 0) return hipMemsetAsync(g.G, 0, sizeof(float) * Dp * Dp, s);
   SolveArgs a{};
-  hipLaunchKernelGGL(wide_syrk_kernel<0>, dim3(xcd_grid(nblk, wide_pairs(Dp))), dim3(256), 0, s, a,
-                     g, Dp, rpb, (int64_t)0, (float*)nullptr, nblk);
+  hipLaunchKernelGGL(wide_syrk2_kernel<0>, dim3(xcd_grid(nblk, wide_pairs2(Dp))), dim3(512), 0, s,
+                     a, g, Dp, rpb, (int64_t)0, (float*)nullptr, nblk);
   hipLaunchKernelGGL(wide_gram_reduce_kernel, dim3((unsigned)(((int64_t)Dp * Dp + 255) / 256)),
                      dim3(256), 0, s, g.partials, nblk, g.G, Dp);
   return hipGetLastError();
@@ -856,7 +880,7 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
   GramArgs g{};
   for (int64_t s0 = 0; s0 < a.n_rows; s0 += batch) {
     const int64_t nb = std::min<int64_t>(batch, a.n_rows - s0);
-    hipLaunchKernelGGL(wide_syrk_kernel<1>, dim3(xcd_grid(nb, wide_pairs(Dp))), dim3(256), 0, s,
+    hipLaunchKernelGGL(wide_syrk2_kernel<1>, dim3(xcd_grid(nb, wide_pairs2(Dp))), dim3(512), 0, s,
                        a, g, Dp, (int64_t)0, s0, ws, nb);
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
