@@ -152,7 +152,7 @@ def path_accounting(ctx, spec, ptrs, timers, K):
     d = spec["dim"]
     Dp = fh.padded_dim(d)
     wide = Dp > 256
-    dual_max, split_rows = 256, 1024
+    dual_max, split_rows = ctx.history_space_max_h(), 1024
     chol = d ** 3 / 3.0 + 2.0 * d * d
     fin_flops, fin_ms, fin_n = 0.0, 0.0, 0
     paths = {}
@@ -162,7 +162,7 @@ def path_accounting(ctx, spec, ptrs, timers, K):
         hs = np.diff(ptr)[lo_:hi_].astype(np.float64)
         hs = hs[hs > 0]
         he = heff_fn(spec["model"], side)(hs)
-        ds = he[he > dual_max] if Dp >= 64 else he
+        ds = he[he > dual_max] if dual_max > 0 else he
         if wide or split_rows <= 0:
             unsplit, split = ds, ds[:0]
         else:
@@ -173,7 +173,7 @@ def path_accounting(ctx, spec, ptrs, timers, K):
             fin_flops += f_fin * n / max(K, 1)
             fin_ms += ms
             fin_n += n
-        hsp = he[he <= dual_max] if Dp >= 64 else he[:0]
+        hsp = he[he <= dual_max] if dual_max > 0 else he[:0]
         hp = 32.0 * np.ceil(hsp / 32.0)
         sp_ms, sp_n = timers[name + ".split"]
         hs_ms, hs_n = timers[name + ".hspace"]

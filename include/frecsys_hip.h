@@ -222,6 +222,9 @@ int frecsys_synchronize(frecsys_ctx* ctx);
 int frecsys_timing(const frecsys_ctx* ctx, const char* what, double* total_ms,
                    int64_t* launches);
 int frecsys_timing_reset(frecsys_ctx* ctx);
+/* Longest assembly history (h_eff) the history-space path takes on this
+ * context (0: that path is off); longer histories run the d-space solve. */
+int32_t frecsys_history_space_max_h(const frecsys_ctx* ctx);
 
 /* ---- diagnostics (tests) ----
  * The basis the history-space solve uses for G[side]: G = Q T Q^T with Q

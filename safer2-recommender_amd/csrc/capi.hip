@@ -129,7 +129,7 @@ struct frecsys_ctx {
   size_t cap_slabs = 0;
   std::vector<int32_t> order_h[3];       // history lengths in queue order
   int dual_on = 1;
-  int dual_max_h = 256;
+  int dual_max_h = 256;  // longest h_eff on the history-space path (set per Dp at create)
   int dual_serial = 0;  // FRECSYS_DUAL_SERIAL=1: no stream overlap (profiling)
   int debug_skip = 0;   // FRECSYS_DEBUG_SKIP ablation mask (-DFRECSYS_ABLATION builds only)
   // per-kernel event pairs, resolved after the call's final synchronisation
@@ -515,6 +515,11 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
       hipEventCreateWithFlags(&c->ev_join3, hipEventDisableTiming) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed (stream2/3)"));
   if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
+  // d-space / history-space crossover: by flops h = d, but at Dp <= 256 the
+  // d-space kernel overtakes the TH = 8 bucket (225 < h <= 256) in time (epoch
+  // 15.6 -> 15.1 ms at the ML-20M shape, threshold sweep in DESIGN.md 3.2); at
+  // Dp = 512 / 1024 the d-space Cholesky is 8x / 64x dearer: keep 256.
+  c->dual_max_h = Dp <= 256 ? 224 : 256;
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H")) c->dual_max_h = atoi(v);
   if (const char* v = getenv("FRECSYS_DUAL_SERIAL")) c->dual_serial = atoi(v);
   if (const char* v = getenv("FRECSYS_SPLIT_ROWS")) c->split_rows = atoi(v);
@@ -1426,6 +1431,10 @@ int frecsys_debug_basis(frecsys_ctx* c, int32_t side, float* q, float* diag, flo
                             c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FRECSYS_OK;
+}
+
+int32_t frecsys_history_space_max_h(const frecsys_ctx* c) {
+  return c && c->dual_on && c->Dp >= 64 ? c->dual_max_h : 0;
 }
 
 int frecsys_timing_reset(frecsys_ctx* c) {

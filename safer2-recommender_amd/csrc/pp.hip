@@ -52,7 +52,10 @@ __global__ void __launch_bounds__(256) pp_block_kernel(PPArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const QueueRec rec = a.order[blockIdx.x];
   const int64_t e = rec.entity, h = rec.h, p0 = rec.p0;
-  if (h == 0) return;
+  if (h == 0) {  // untouched entity: its residual slot is read by the host sum
+    if (tid == 0 && a.resid) a.resid[blockIdx.x] = 0.0f;
+    return;
+  }
   const int Dp = a.Dp, s0 = a.start, bw = a.bw, kind = a.kind;
   const bool uk = kind == KIND_WEIGHTED_U, vk = kind == KIND_WEIGHTED_V;
   // RegularizationValue (ialspp.h:313-318) / User-, ItemRegularizationValue

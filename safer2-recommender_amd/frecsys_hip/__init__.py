@@ -37,6 +37,7 @@ EXPORTS = (
     "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset", "frecsys_debug_basis",
     "frecsys_eval_topk", "frecsys_train_stats", "frecsys_pp_set_rating_index",
     "frecsys_pp_predict", "frecsys_pp_step", "frecsys_debug_diag_factor",
+    "frecsys_history_space_max_h",
 )
 
 # Every symbol include/frecsys_model.h declares.
@@ -120,6 +121,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_synchronize": (ctypes.c_int, [P]),
         "frecsys_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, P]),
         "frecsys_timing_reset": (ctypes.c_int, [P]),
+        "frecsys_history_space_max_h": (I32, [P]),
         "frecsys_debug_basis": (ctypes.c_int, [P, I32, P, P, P]),
         "frecsys_debug_diag_factor": (ctypes.c_int, [P, I32, I32, P, P, P]),
         "frecsys_eval_topk": (ctypes.c_int, [P, I32, P]),
@@ -321,6 +323,9 @@ class Context:
         self._check(self.lib.frecsys_timing(self.h, what.encode(), ctypes.byref(ms),
                                             ctypes.byref(n)))
         return float(ms.value), int(n.value)
+
+    def history_space_max_h(self) -> int:
+        return int(self.lib.frecsys_history_space_max_h(self.h))
 
     def timing_reset(self):
         self._check(self.lib.frecsys_timing_reset(self.h))

@@ -141,6 +141,7 @@ def test_tail_quirk_in_history_space(monkeypatch, quirk_data):
     """Quirk rows (A only, not b) must matter in the history-space form too."""
     nu, ni, up, uc, ip, ic = quirk_data
     monkeypatch.setenv("FRECSYS_DUAL", "1")
+    monkeypatch.setenv("FRECSYS_DUAL_MAX_H", "256")  # h_eff = 256 rows in history space
     dim = 64
     om = _weights(nu)
     nu_w, item_reg = _v_inputs(nu, ni, up, ip, ic, om)
@@ -194,7 +195,9 @@ def test_every_bucket_filled_and_solved(quirk_data, monkeypatch):
     assert all(c > 0 for c in _buckets(hi)), _buckets(hi)
     assert (hu > 256).any() and (hi > 256).any()
     dim = 256
+    monkeypatch.setenv("FRECSYS_DUAL_MAX_H", "256")  # TH = 8 too (the d=256 default is 224)
     ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+    assert ctx.history_space_max_h() == 256
     reg, w = 0.003, 0.1
     ctx.gramian(fh.SIDE_ITEM)
     ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, reg, w)
@@ -209,3 +212,14 @@ def test_every_bucket_filled_and_solved(quirk_data, monkeypatch):
     Vo, rc = O.step(ip, ic, Uo, O.gramian(Uo), 0, reg, w, out=V.copy())
     assert rc == 0
     assert rel_rows(ctx.get_embeddings(fh.SIDE_ITEM), Vo).max() < TOL_ROW
+
+
+@pytest.mark.parametrize("dim,expect", [(32, 0), (64, 224), (256, 224), (512, 256), (1024, 256)])
+def test_default_history_space_threshold(quirk_data, dim, expect):
+    """Crossover of the two paths (capi.hip): h_eff <= 224 at Dp <= 256 (the
+    d-space kernel is faster for the TH = 8 bucket there), 256 at the wide
+    dims; no history-space path below Dp = 64."""
+    nu, ni, up, uc, ip, ic = quirk_data
+    ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+    assert ctx.history_space_max_h() == expect
+    ctx.close()
