@@ -91,6 +91,8 @@ struct frecsys_ctx {
   float* tri[2] = {nullptr, nullptr};    // [2 * Dp]: diagonal, subdiagonal
   float* refl[2] = {nullptr, nullptr};   // Dp x Dp reflectors + [Dp] tau
   float* xrot[2] = {nullptr, nullptr};   // n_s x Dp
+  void* qsplit[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};  // split images of Q, Q^T
+  void* gsplit = nullptr;  // split image of G[ITEM] for the wide user loss
   float* out_rot[3] = {nullptr, nullptr, nullptr};
   size_t cap_xrot[2] = {0, 0};
   size_t cap_out_rot[3] = {0, 0, 0};
@@ -320,7 +322,11 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
   HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp, c->refl[other],
                             tau, s, c->tri_work));
   HIP_TRY(c, launch_form_q(c->refl[other], tau, Dp, c->q[other], s));
-  HIP_TRY(c, launch_rot_gemm(X, nullptr, 0, c->n[other], c->q[other], 0, c->xrot[other], Dp, s));
+  for (int t = 0; t < 2; ++t) {  // bf16-piece images of Q (forward) and Q^T (back)
+    if (!c->qsplit[other][t]) HIP_TRY(c, hipMalloc(&c->qsplit[other][t], basis_split_bytes(Dp)));
+    HIP_TRY(c, launch_split_basis(c->q[other], Dp, t, c->qsplit[other][t], s));
+  }
+  HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp, s));
   return FRECSYS_OK;
 }
 
@@ -576,9 +582,13 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (c->d_counter) (void)hipFree(c->d_counter);
   for (int s = 0; s < 3; ++s)
     if (c->d_order[s]) (void)hipFree(c->d_order[s]);
-  for (int s = 0; s < 2; ++s)
+  for (int s = 0; s < 2; ++s) {
     for (float* p : {c->q[s], c->tri[s], c->refl[s], c->xrot[s]})
       if (p) (void)hipFree(p);
+    for (void* p : c->qsplit[s])
+      if (p) (void)hipFree(p);
+  }
+  if (c->gsplit) (void)hipFree(c->gsplit);
   for (int s = 0; s < 3; ++s)
     if (c->out_rot[s]) (void)hipFree(c->out_rot[s]);
   if (c->dual_table) (void)hipFree(c->dual_table);
@@ -1040,8 +1050,8 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       HIP_TRY(c, launch_dual_sweep(d, c->stream));
       ktimer_end(c, k, c->stream);
       k = ktimer_begin(c, pre + ".rotate", c->stream);
-      HIP_TRY(c, launch_rot_gemm(c->out_rot[side], a.order + n_dspace, 0, n_nonempty - n_dspace,
-                                 c->q[other], 1, a.out, c->Dp, c->stream, 1));
+      HIP_TRY(c, launch_rotate(c->out_rot[side], a.order + n_dspace, 0, n_nonempty - n_dspace,
+                               c->qsplit[other][1], a.out, c->Dp, c->stream, 1));
       ktimer_end(c, k, c->stream);
       if (n_dspace > 0) HIP_TRY(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
     }
@@ -1116,6 +1126,10 @@ int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, fl
   if (rc) return rc;
   LossArgs a{};
   a.quad = c->d_quad;
+  if (wide_dim(c->Dp)) {
+    if (!c->gsplit) HIP_TRY(c, hipMalloc(&c->gsplit, basis_split_bytes(c->Dp)));
+    a.gsplit = c->gsplit;
+  }
   a.row_ptr = c->rp[side];
   a.col = c->col[side];
   a.row_lo = lo;

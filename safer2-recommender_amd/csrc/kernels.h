@@ -74,6 +74,7 @@ struct LossArgs {
   int half;
   float* out;            // [rows of side]
   float* quad;           // [rows of side] scratch: u^T G u (Dp >= 32)
+  void* gsplit;          // Dp = 512 / 1024: scratch for G's split image (basis_split_bytes)
   int raw;               // 1: out[e] = sum_j (x_j . u - 1)^2 only (train stats)
 };
 
@@ -143,13 +144,21 @@ hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, flo
                           float* tau, hipStream_t s, float* work = nullptr);
 // Q = H_0 H_1 ... H_{Dp-3} from the reflectors, row-major Dp x Dp.
 hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s);
-// Y[row] = X[row] * (trans ? Q^T : Q) for rows r0..r0+n-1, or for the
-// entities rows[0..n) when rows != nullptr.  Y: ld Dp; X: ld Dp, or with
-// x_blocked the position-blocked layout of DualArgs::out_rot (X row r =
-// position r).
-hipError_t launch_rot_gemm(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
-                           const float* Q, int trans, float* Y, int Dp, hipStream_t s,
-                           int x_blocked = 0);
+// The split image of B = (trans ? Q^T : Q) for launch_rotate: Dp * Dp * 3
+// bf16 (16-B granules in MFMA fragment order).
+size_t basis_split_bytes(int Dp);
+hipError_t launch_split_basis(const float* Q, int Dp, int trans, void* out, hipStream_t s);
+// Y[row] = X[row] * B with B given by its split image (launch_split_basis),
+// fp32-accurate products on the bf16 matrix cores,
+// for rows r0..r0+n-1, or for the entities rows[0..n) when rows != nullptr
+// (Y: ld Dp; X: ld Dp, or with x_blocked the position-blocked layout of
+// DualArgs::out_rot, X row r = position r).  Dp = 64 .. 256, 512, 1024.
+hipError_t launch_rotate(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
+                         const void* bsplit, float* Y, int Dp, hipStream_t s, int x_blocked = 0);
+// Dp = 512 / 1024: qpart[b * n + r] = sum over the columns of 128-block b of
+// (X B)[r] .* X[r] for rows r0 .. r0+n-1 (u^T G u partials, B = G).
+hipError_t launch_rotate_quad(const float* X, int64_t r0, int64_t n, const void* bsplit,
+                              float* qpart, int Dp, hipStream_t s);
 
 __host__ __device__ inline int64_t blk_v(int64_t p, int k, int Dp) {
   return ((p >> 6) * Dp + k) * 64 + (p & 63);
@@ -204,9 +213,6 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
 size_t wide_tridiag_work_floats(int Dp);
 hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
                                float* tau, float* work, hipStream_t s);
-hipError_t launch_wide_rot(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
-                           const float* Q, int trans, float* Y, int Dp, hipStream_t s,
-                           int x_blocked);
 size_t wide_quad_floats(int Dp, int64_t rows);
 hipError_t launch_wide_user_loss(int Dp, const LossArgs& a, hipStream_t s);
 hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s);

@@ -11,9 +11,10 @@
 //                  matrix in registers (an 8 x 8 block per thread), LAPACK
 //                  sytd2 conventions (v(k+1) = 1).
 //  form_q_kernel   Q = H_0 ... H_{n-3}, one wave per column of Q.
-//  rot_gemm_kernel 64 rows x Dp columns per workgroup, v_mfma_f32_32x32x2_f32,
-//                  the row block in LDS and Q streamed through LDS by 32-row
-//                  slabs; optional entity list for gather/scatter.
+//  rotate_kernel   Y = X Q / X Q^T on the bf16 matrix cores (3-piece splits,
+//                  fp32-accurate), Q split once per basis (split_basis_kernel);
+//                  optional entity list for the scatter; also the u^T G u
+//                  partials of the wide user loss.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -357,95 +358,150 @@ __global__ void __launch_bounds__(512)
   }
 }
 
-// Y = X B, B = Q or Q^T; 64 rows per workgroup, 4 waves, tiles of 32x32.
-template <int NCT>
+// ---- rotations on the bf16 matrix cores ----
+// Y = X B (B = Q or Q^T), fp32-accurate: every product as common.h mfma_x6
+// (3-piece bf16 splits).  B is split once per basis into its fragment image
+// (split_basis_kernel): granule ((s * NCT + C) * 3 + p) * 64 + lane holds
+// piece p of B[16s + 8hi .. +7][32C + lo] (lane = 32 hi + lo) -- one 1-KB
+// coalesced load per wave and MFMA operand, L2-resident (Dp^2 * 6 bytes).
+// X rows go straight from global memory into the A fragments (2 float4 per
+// lane and k16 step, or 8 position-blocked scalars), so the kernel uses no
+// LDS.  A workgroup: 4 waves, 64 rows x (2 or 4) 32-column tiles; the column
+// blocks of one row block sit on one XCD (consecutive slots of its dispatch
+// sequence) so X's rows are fetched from HBM once.
 __global__ void __launch_bounds__(256)
-    rot_gemm_kernel(const float* __restrict__ X, const QueueRec* __restrict__ rows, int64_t r0,
-                    int64_t n, const float* __restrict__ Q, int trans, float* __restrict__ Y,
-                    int x_blocked) {
-  constexpr int Dp = 32 * NCT, XS = Dp + 1;
-  constexpr int NTILE = 2 * NCT, MT = (NTILE + 3) / 4;
-  __shared__ float xs[64 * XS];
-  __shared__ float bs[32 * Dp];
-  __shared__ int64_t rid[64];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lo = lane & 31, hi = lane >> 5;
-  const int64_t base = (int64_t)blockIdx.x * 64;
-  if (tid < 64) {
-    const int64_t r = base + tid;
-    rid[tid] = r < n ? (rows ? (int64_t)rows[r].entity : r0 + r) : -1;
+    split_basis_kernel(const float* __restrict__ Q, int DP, int trans, bf16x8* __restrict__ out) {
+  const int NCT = DP / 32, NS = DP / 16;
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (int64_t)NS * NCT * 64) return;
+  const int lane = (int)(g & 63), lo = lane & 31, hi = lane >> 5;
+  const int64_t sc = g >> 6;
+  const int C = (int)(sc % NCT), s = (int)(sc / NCT);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 16 * s + 8 * hi + j, col = 32 * C + lo;
+    v[j] = trans ? Q[(int64_t)col * DP + k] : Q[(int64_t)k * DP + col];
   }
-  __syncthreads();
-  if (x_blocked) {  // rows = positions base .. base+63 = one 64-position block
-    const float* xb = X + base * Dp;
-    for (int s = tid; s < 64 * Dp; s += 256) xs[(s & 63) * XS + (s >> 6)] = xb[s];
-  } else {
-    for (int s = tid; s < 64 * (Dp / 4); s += 256) {
-      const int rr = s / (Dp / 4), c4 = s % (Dp / 4);
-      const int64_t id = rid[rr];
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (id >= 0) v = *reinterpret_cast<const float4*>(X + id * Dp + 4 * c4);
-      float* d = xs + rr * XS + 4 * c4;
-      d[0] = v.x;
-      d[1] = v.y;
-      d[2] = v.z;
-      d[3] = v.w;
+  bf16x8 f[3];
+  split3x8(v, f);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) out[(sc * 3 + p) * 64 + lane] = f[p];
+}
+
+template <int DP>
+__global__ void __launch_bounds__(256)
+    rotate_kernel(const float* __restrict__ X, const QueueRec* __restrict__ rows, int64_t r0,
+                  int64_t n, const bf16x8* __restrict__ Bs, float* __restrict__ Y, int x_blocked,
+                  int ncb, float* __restrict__ qpart) {
+  constexpr int NCT = DP / 32, NS = DP / 16;
+  constexpr int CW = (DP % 128 == 0) ? 2 : 1;  // column tiles per wave
+  constexpr int CB = 2 * CW;                   // column tiles per workgroup
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // slot b -> XCD b % 8; the ncb column blocks of a row block on one XCD
+  const int64_t bid = blockIdx.x, sx = bid >> 3;
+  const int cbk = (int)(sx % ncb);
+  const int64_t rblk = (sx / ncb) * 8 + (bid & 7);
+  const int64_t base = rblk * 64;
+  if (base >= n) return;
+  const int R = wave & 1, cg = wave >> 1;
+  const int C0 = cbk * CB + cg * CW;
+  const int64_t pos = base + 32 * R + lo;  // my A row (position)
+  const bool pv = pos < n;
+  const float* xr = X + (x_blocked ? 0 : (r0 + (pv ? pos : base)) * DP);
+  f32x16 acc[CW];
+#pragma unroll
+  for (int j = 0; j < CW; ++j) acc[j] = f32x16{0.f};
+  auto load_a = [&](int s, float (&v)[8]) {
+    const int k0 = 16 * s + 8 * hi;
+    if (x_blocked) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = pv ? X[blk_v(pos, k0 + j, DP)] : 0.0f;
+    } else {
+      const float4 a = *reinterpret_cast<const float4*>(xr + k0);
+      const float4 b = *reinterpret_cast<const float4*>(xr + k0 + 4);
+      v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w;
+      v[4] = b.x, v[5] = b.y, v[6] = b.z, v[7] = b.w;
+      if (!pv) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+      }
+    }
+  };
+  float vn[8];
+  load_a(0, vn);
+#pragma unroll 4
+  for (int s = 0; s < NS; ++s) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = vn[j];
+    if (s + 1 < NS) load_a(s + 1, vn);  // next step's rows in flight
+    bf16x8 af[3];
+    split3x8(v, af);
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const int C = C0 + j;
+      if (C < NCT) {  // wave-uniform
+        bf16x8 bf[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bf[p] = Bs[((int64_t)(s * NCT + C) * 3 + p) * 64 + lane];
+        acc[j] = mfma_x6(af, bf, acc[j]);
+      }
     }
   }
-  f32x16 acc[MT];
+  if (qpart) {
+    // u^T B u partials of the user loss (B = G): row dots of (X B) with X
+    // over this workgroup's column block, two waves per row half combined in
+    // a fixed order -> qpart[column block][row]
+    __shared__ float qred[2][64];
+    float rs[16];
 #pragma unroll
-  for (int m = 0; m < MT; ++m) acc[m] = f32x16{0.f};
-  for (int c = 0; c < NCT; ++c) {
-    __syncthreads();  // xs ready / previous slab consumed
-    if (!trans) {
-      for (int s = tid; s < 32 * (Dp / 4); s += 256) {
-        const int kk = s / (Dp / 4), c4 = s % (Dp / 4);
-        *reinterpret_cast<float4*>(bs + kk * Dp + 4 * c4) =
-            *reinterpret_cast<const float4*>(Q + (int64_t)(32 * c + kk) * Dp + 4 * c4);
+    for (int q = 0; q < 16; ++q) {
+      const int64_t p = base + 32 * R + acc_row(q, hi);
+      float sv = 0.0f;
+      if (p < n) {
+#pragma unroll
+        for (int j = 0; j < CW; ++j)
+          if (C0 + j < NCT) sv += acc[j][q] * X[(r0 + p) * DP + 32 * (C0 + j) + lo];
       }
-    } else {  // bs[kk][j] = Q[j][32c + kk]
-      for (int s = tid; s < Dp * 8; s += 256) {
-        const int j = s >> 3, k4 = s & 7;
-        const float4 v = *reinterpret_cast<const float4*>(Q + (int64_t)j * Dp + 32 * c + 4 * k4);
-        bs[(4 * k4 + 0) * Dp + j] = v.x;
-        bs[(4 * k4 + 1) * Dp + j] = v.y;
-        bs[(4 * k4 + 2) * Dp + j] = v.z;
-        bs[(4 * k4 + 3) * Dp + j] = v.w;
-      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) sv += __shfl_xor(sv, o);  // the 32 columns of a half
+      rs[q] = sv;
+    }
+    if (lo == 0) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) qred[cg][32 * R + acc_row(q, hi)] = rs[q];
     }
     __syncthreads();
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int t = wave + 4 * m;
-      if (t < NTILE) {
-        const int R = t & 1, C = t >> 1;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const int kk = 2 * s + hi;
-          acc[m] = mfma32(xs[(32 * R + lo) * XS + 32 * c + kk], bs[kk * Dp + 32 * C + lo], acc[m]);
-        }
-      }
-    }
+    if (tid < 64 && base + tid < n) qpart[(int64_t)cbk * n + base + tid] = qred[0][tid] + qred[1][tid];
+    return;
   }
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    const int t = wave + 4 * m;
-    if (t < NTILE) {
-      const int R = t & 1, C = t >> 1;
+  for (int j = 0; j < CW; ++j) {
+    const int C = C0 + j;
+    if (C >= NCT) continue;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int64_t id = rid[32 * R + acc_row(q, hi)];
-        if (id >= 0) Y[id * Dp + 32 * C + lo] = acc[m][q];
+    for (int q = 0; q < 16; ++q) {
+      const int64_t p = base + 32 * R + acc_row(q, hi);
+      if (p < n) {
+        const int64_t id = rows ? (int64_t)rows[p].entity : r0 + p;
+        Y[id * DP + 32 * C + lo] = acc[j][q];
       }
     }
   }
 }
 
-template <int NCT>
-hipError_t launch_rot(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
-                      const float* Q, int trans, float* Y, hipStream_t s, int xb) {
-  const unsigned nb = (unsigned)((n + 63) / 64);
-  hipLaunchKernelGGL(rot_gemm_kernel<NCT>, dim3(nb), dim3(256), 0, s, X, rows, r0, n, Q, trans, Y,
-                     xb);
+template <int DP>
+hipError_t launch_rotate_t(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
+                           const bf16x8* Bs, float* Y, hipStream_t s, int xb,
+                           float* qpart = nullptr) {
+  constexpr int CB = (DP % 128 == 0) ? 4 : 2;
+  const int ncb = (DP / 32 + CB - 1) / CB;
+  const int64_t units = (n + 63) / 64;
+  const unsigned grid = (unsigned)(((units + 7) / 8) * 8 * ncb);
+  hipLaunchKernelGGL(rotate_kernel<DP>, dim3(grid), dim3(256), 0, s, X, rows, r0, n, Bs, Y, xb,
+                     ncb, qpart);
   return hipGetLastError();
 }
 
@@ -471,21 +527,41 @@ hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hi
   return hipGetLastError();
 }
 
-hipError_t launch_rot_gemm(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
-                           const float* Q, int trans, float* Y, int Dp, hipStream_t s,
-                           int x_blocked) {
+size_t basis_split_bytes(int Dp) { return (size_t)Dp * Dp * 3 * sizeof(__bf16); }
+
+hipError_t launch_split_basis(const float* Q, int Dp, int trans, void* out, hipStream_t s) {
+  if (Dp < 64 || Dp % 32 != 0) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)(Dp / 16) * (Dp / 32) * 64;
+  hipLaunchKernelGGL(split_basis_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, Q, Dp,
+                     trans, reinterpret_cast<bf16x8*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_rotate(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
+                         const void* bsplit, float* Y, int Dp, hipStream_t s, int x_blocked) {
   if (n <= 0) return hipSuccess;
-  if (wide_dim(Dp)) return launch_wide_rot(X, rows, r0, n, Q, trans, Y, Dp, s, x_blocked);
+  const bf16x8* B = reinterpret_cast<const bf16x8*>(bsplit);
   switch (Dp) {
-    case 64: return launch_rot<2>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
-    case 96: return launch_rot<3>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
-    case 128: return launch_rot<4>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
-    case 160: return launch_rot<5>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
-    case 192: return launch_rot<6>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
-    case 224: return launch_rot<7>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
-    case 256: return launch_rot<8>(X, rows, r0, n, Q, trans, Y, s, x_blocked);
+    case 64: return launch_rotate_t<64>(X, rows, r0, n, B, Y, s, x_blocked);
+    case 96: return launch_rotate_t<96>(X, rows, r0, n, B, Y, s, x_blocked);
+    case 128: return launch_rotate_t<128>(X, rows, r0, n, B, Y, s, x_blocked);
+    case 160: return launch_rotate_t<160>(X, rows, r0, n, B, Y, s, x_blocked);
+    case 192: return launch_rotate_t<192>(X, rows, r0, n, B, Y, s, x_blocked);
+    case 224: return launch_rotate_t<224>(X, rows, r0, n, B, Y, s, x_blocked);
+    case 256: return launch_rotate_t<256>(X, rows, r0, n, B, Y, s, x_blocked);
+    case 512: return launch_rotate_t<512>(X, rows, r0, n, B, Y, s, x_blocked);
+    case 1024: return launch_rotate_t<1024>(X, rows, r0, n, B, Y, s, x_blocked);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_rotate_quad(const float* X, int64_t r0, int64_t n, const void* bsplit,
+                              float* qpart, int Dp, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const bf16x8* B = reinterpret_cast<const bf16x8*>(bsplit);
+  if (Dp == 512) return launch_rotate_t<512>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+  if (Dp == 1024) return launch_rotate_t<1024>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+  return hipErrorInvalidValue;
 }
 
 }  // namespace frecsys_hip

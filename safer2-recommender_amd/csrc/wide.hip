@@ -31,9 +31,8 @@
 //                        matrix), re-forms the step's reflector from the
 //                        updated row k itself, and writes its columns of
 //                        p = tau A v for the next launch.
-//   rot_wide_kernel      Y = X Q / X Q^T, 64 rows x 128 columns per
-//                        workgroup, K streamed in 32-wide slabs; also the
-//                        u^T G u partials of the user loss.
+//   rotations            spectral.hip rotate_kernel (split-bf16), which also
+//                        forms the u^T G u partials of the user loss.
 // and the Gramian: wide_syrk2_kernel<0> (split-K over row blocks x block
 // pairs) + wide_gram_reduce_kernel (fixed order, deterministic).
 #include <hip/hip_runtime.h>
@@ -681,100 +680,9 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Y = X B (B = Q, or Q^T with trans) for 64 rows x 128 columns per
-// workgroup; with qpart, instead the partial row dots sum_c (X G)[r][c] X[r][c]
-// over the block's columns (u^T G u, summed over blocks by the loss).
-__global__ void __launch_bounds__(256)
-    rot_wide_kernel(const float* __restrict__ X, const QueueRec* __restrict__ rows, int64_t r0,
-                    int64_t n, const float* __restrict__ Q, int trans, float* __restrict__ Y,
-                    int x_blocked, int Dp, float* __restrict__ qpart) {
-  __shared__ float xs[64 * 33];
-  __shared__ float bs[32 * (WB + 1)];
-  __shared__ int64_t rid[64];
-  __shared__ float qred[2][64];
-  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t base = (int64_t)blockIdx.x * 64;
-  const int cb = blockIdx.y;
-  if (tid < 64) {
-    const int64_t r = base + tid;
-    rid[tid] = r < n ? (rows ? (int64_t)rows[r].entity : r0 + r) : -1;
-  }
-  __syncthreads();
-  const int R = wave & 1, Cs = (wave >> 1) * 2;
-  f32x16 acc[2] = {f32x16{0.f}, f32x16{0.f}};
-  const int NC = Dp >> 5;
-  for (int c = 0; c < NC; ++c) {
-    __syncthreads();
-    if (x_blocked) {
-      const float* xb = X + ((base >> 6) * Dp + 32 * c) * 64;
-      for (int s = tid; s < 64 * 32; s += 256) xs[(s & 63) * 33 + (s >> 6)] = xb[s];
-    } else {
-      for (int s = tid; s < 64 * 32; s += 256) {
-        const int rr = s >> 5, kk = s & 31;
-        const int64_t id = rid[rr];
-        xs[rr * 33 + kk] = id >= 0 ? X[id * Dp + 32 * c + kk] : 0.0f;
-      }
-    }
-    if (!trans) {
-      for (int s = tid; s < 32 * WB; s += 256) {
-        const int kk = s >> 7, j = s & 127;
-        bs[kk * (WB + 1) + j] = Q[(int64_t)(32 * c + kk) * Dp + WB * cb + j];
-      }
-    } else {
-      for (int s = tid; s < 32 * WB; s += 256) {
-        const int j = s >> 5, kk = s & 31;
-        bs[kk * (WB + 1) + j] = Q[(int64_t)(WB * cb + j) * Dp + 32 * c + kk];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int C = Cs + t;
-#pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) {
-        const int kk = 2 * s2 + hi;
-        acc[t] = mfma32(xs[(32 * R + lo) * 33 + kk], bs[kk * (WB + 1) + 32 * C + lo], acc[t]);
-      }
-    }
-  }
-  if (!qpart) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int C = Cs + t;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int64_t id = rid[32 * R + acc_row(q, hi)];
-        if (id >= 0) Y[id * Dp + WB * cb + 32 * C + lo] = acc[t][q];
-      }
-    }
-    return;
-  }
-  // row dots with X over this block's 128 columns
-  float rs[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int64_t id = rid[32 * R + acc_row(q, hi)];
-    float s = 0.0f;
-    if (id >= 0) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) s += acc[t][q] * X[id * Dp + WB * cb + 32 * (Cs + t) + lo];
-    }
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o);  // over the 32 columns of a half
-    rs[q] = s;
-  }
-  if (lo == 0) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) qred[wave >> 1][32 * R + acc_row(q, hi)] = rs[q];
-  }
-  __syncthreads();
-  if (tid < 64 && base + tid < n) qpart[(int64_t)cb * n + base + tid] = qred[0][tid] + qred[1][tid];
-}
-
 // User loss at wide Dp: one wave per user, Dp/32 lanes per history row
-// (8 float4 each), 64*32/Dp rows in flight; u^T G u from the rot_wide_kernel
-// partials summed in column-block order.
+// (8 float4 each), 64*32/Dp rows in flight; u^T G u from the rotate_kernel
+// partials (one per 128-column block) summed in column-block order.
 template <int Dp>
 __global__ void __launch_bounds__(256) loss_gather_wide_kernel(LossArgs a) {
   constexpr int LPR = Dp / 32, NG = 64 / LPR, NB = Dp / WB;
@@ -908,27 +816,18 @@ hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff
   return hipGetLastError();
 }
 
-hipError_t launch_wide_rot(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
-                           const float* Q, int trans, float* Y, int Dp, hipStream_t s,
-                           int x_blocked) {
-  if (!wide_dim(Dp)) return hipErrorInvalidValue;
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rot_wide_kernel, dim3((unsigned)((n + 63) / 64), (unsigned)(Dp / WB)),
-                     dim3(256), 0, s, X, rows, r0, n, Q, trans, Y, x_blocked, Dp,
-                     (float*)nullptr);
-  return hipGetLastError();
-}
 
 size_t wide_quad_floats(int Dp, int64_t rows) { return (size_t)(Dp / WB) * (size_t)rows; }
 
 hipError_t launch_wide_user_loss(int Dp, const LossArgs& a, hipStream_t s) {
   if (!wide_dim(Dp)) return hipErrorInvalidValue;
   if (a.n_rows <= 0) return hipSuccess;
-  if (!a.raw)
-    hipLaunchKernelGGL(rot_wide_kernel,
-                       dim3((unsigned)((a.n_rows + 63) / 64), (unsigned)(Dp / WB)), dim3(256), 0,
-                       s, a.U, (const QueueRec*)nullptr, a.row_lo, a.n_rows, a.G, 0,
-                       (float*)nullptr, 0, Dp, a.quad);
+  if (!a.raw) {  // u^T G u partials: (U G) .* U on the bf16 matrix cores (spectral.hip)
+    hipError_t e = launch_split_basis(a.G, Dp, 0, a.gsplit, s);
+    if (e != hipSuccess) return e;
+    e = launch_rotate_quad(a.U, a.row_lo, a.n_rows, a.gsplit, a.quad, Dp, s);
+    if (e != hipSuccess) return e;
+  }
   const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
   if (Dp == 512)
     hipLaunchKernelGGL(loss_gather_wide_kernel<512>, dim3(nb), dim3(256), 0, s, a);
