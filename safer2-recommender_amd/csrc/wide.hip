@@ -591,40 +591,72 @@ __global__ void __launch_bounds__(256)
 // workgroup re-forms row k of the updated matrix and reflector k from it;
 // workgroup b then updates columns [16b, 16b+16) into Aout (rows >= k+1)
 // and writes those columns of p_k = tau_k A v_k to pout.
+template <int N>
 __global__ void __launch_bounds__(256)
-    tridiag_step_kernel(const float* __restrict__ Ain, float* __restrict__ Aout, int n, int k,
+    tridiag_step_kernel(const float* __restrict__ Ain, float* __restrict__ Aout, int k,
                         const float* __restrict__ pin, float* __restrict__ pout,
                         float* __restrict__ Vh, float* __restrict__ tau,
                         float* __restrict__ tdiag, float* __restrict__ toff) {
-  constexpr int CW = 16;
+  constexpr int n = N, CW = 16, NR = N / 16, NV = N / 256;
   const int c0 = blockIdx.x * CW;
   if (blockIdx.x != 0 && c0 + CW <= k + 1) return;  // whole workgroup, before any barrier
-  __shared__ float vp[1024], wv[1024], vk[1024];
+  __shared__ float vp[N], wv[N], vk[N];
   __shared__ float red[8];
   __shared__ float pc[16][CW + 1];
   const int tid = threadIdx.x;
-  // previous reflector and w
+  const int c = c0 + (tid & (CW - 1)), rg = tid >> 4;
+  // ---- every global load of the step, issued at entry: the previous
+  // reflector, p, row k, and this thread's strip of its column (rows rg,
+  // rg + 16, ...) -- one memory round trip instead of a chain of them ----
   const float tp = k > 0 ? tau[k - 1] : 0.0f;
-  for (int r = tid; r < n; r += 256) {
+  float vpr[NV], pir[NV], akr[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int r = tid + 256 * j;
+    vpr[j] = (k > 0 && r > k) ? Vh[(int64_t)(k - 1) * n + r] : 0.0f;
+    pir[j] = r >= k ? pin[r] : 0.0f;
+    akr[j] = r >= k ? Ain[(int64_t)k * n + r] : 0.0f;
+  }
+  const bool col_live = c >= k + 1 && c < n && k + 1 < n;
+  float sreg[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = rg + 16 * i;
+    sreg[i] = (col_live && r >= k + 1) ? Ain[(int64_t)r * n + c] : 0.0f;
+  }
+  // previous reflector and w
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int r = tid + 256 * j;
     float v = 0.0f;
-    if (k > 0 && tp != 0.0f) v = r == k ? 1.0f : (r > k ? Vh[(int64_t)(k - 1) * n + r] : 0.0f);
+    if (k > 0 && tp != 0.0f) v = r == k ? 1.0f : vpr[j];
     vp[r] = v;
   }
   __syncthreads();
   float d = 0.0f;
-  if (tp != 0.0f)
-    for (int r = k + tid; r < n; r += 256) d += pin[r] * vp[r];
+  if (tp != 0.0f) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) d += pir[j] * vp[tid + 256 * j];
+  }
   d = block_sum(d, red);
   const float K = -0.5f * tp * d;
-  for (int r = tid; r < n; r += 256) wv[r] = (tp != 0.0f && r >= k) ? pin[r] + K * vp[r] : 0.0f;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int r = tid + 256 * j;
+    wv[r] = (tp != 0.0f && r >= k) ? pir[j] + K * vp[r] : 0.0f;
+  }
   __syncthreads();
   // row k of the updated matrix -> reflector k
   const float vpk = vp[k], wk = wv[k];
   float xn = 0.0f;
-  for (int r = k + tid; r < n; r += 256) {
-    const float ck = Ain[(int64_t)k * n + r] - vpk * wv[r] - wk * vp[r];
-    vk[r] = ck;
-    if (r >= k + 2) xn += ck * ck;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int r = tid + 256 * j;
+    if (r >= k) {
+      const float ck = akr[j] - vpk * wv[r] - wk * vp[r];
+      vk[r] = ck;
+      if (r >= k + 2) xn += ck * ck;
+    }
   }
   xn = block_sum(xn, red);  // (barriers inside: vk complete)
   const float dkk = vk[k];
@@ -641,7 +673,9 @@ __global__ void __launch_bounds__(256)
     }
   }
   __syncthreads();
-  for (int r = tid; r < n; r += 256) {
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int r = tid + 256 * j;
     float v = 0.0f;
     if (r == k + 1) v = 1.0f;
     else if (r >= k + 2) v = tk != 0.0f ? vk[r] * scal : 0.0f;
@@ -659,24 +693,27 @@ __global__ void __launch_bounds__(256)
   }
   if (k + 1 >= n) return;
   // my columns: finish step k-1's update (rows >= k+1) and p_k
-  const int c = c0 + (tid & (CW - 1)), rg = tid >> 4;
   float pacc = 0.0f;
-  if (c >= k + 1 && c < n) {
+  if (col_live) {
     const float vpc = vp[c], wc = wv[c];
-    for (int r = k + 1 + rg; r < n; r += 16) {
-      const float v = Ain[(int64_t)r * n + c] - vp[r] * wc - wv[r] * vpc;
-      Aout[(int64_t)r * n + c] = v;
-      pacc += v * vk[r];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int r = rg + 16 * i;
+      if (r >= k + 1) {
+        const float v = sreg[i] - vp[r] * wc - wv[r] * vpc;
+        Aout[(int64_t)r * n + c] = v;
+        pacc += v * vk[r];
+      }
     }
   }
   pc[rg][tid & (CW - 1)] = pacc;
   __syncthreads();
   if (tid < CW) {
     const int cc = c0 + tid;
-    float s = 0.0f;
+    float sum = 0.0f;
 #pragma unroll
-    for (int g2 = 0; g2 < 16; ++g2) s += pc[g2][tid];
-    if (cc >= k + 1 && cc < n) pout[cc] = tk * s;
+    for (int g2 = 0; g2 < 16; ++g2) sum += pc[g2][tid];
+    if (cc >= k + 1 && cc < n) pout[cc] = tk * sum;
   }
 }
 
@@ -810,8 +847,12 @@ hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff
   const unsigned nb = (unsigned)((n + 15) / 16);
   for (int k = 0; k < n; ++k) {
     const float* ain = k == 0 ? G : A[(k - 1) & 1];
-    hipLaunchKernelGGL(tridiag_step_kernel, dim3(nb), dim3(256), 0, s, ain, A[k & 1], n, k,
-                       (const float*)P[(k + 1) & 1], P[k & 1], Vh, tau, tdiag, toff);
+    if (n == 512)
+      hipLaunchKernelGGL(tridiag_step_kernel<512>, dim3(nb), dim3(256), 0, s, ain, A[k & 1], k,
+                         (const float*)P[(k + 1) & 1], P[k & 1], Vh, tau, tdiag, toff);
+    else
+      hipLaunchKernelGGL(tridiag_step_kernel<1024>, dim3(nb), dim3(256), 0, s, ain, A[k & 1], k,
+                         (const float*)P[(k + 1) & 1], P[k & 1], Vh, tau, tdiag, toff);
   }
   return hipGetLastError();
 }
