@@ -39,16 +39,39 @@ __device__ __forceinline__ float rdlane(float v, int l) {
 // ---------------------------------------------------------------------
 typedef __attribute__((address_space(3))) float lds_float;
 
+// Lanes 0..31: row r of the swizzled tile; lanes 32..63: column r of the
+// identity.  The reads are issued G at a time before a wait (both halves
+// read: no divergent loads; the asm keeps the select below after the loads
+// instead of turning it into per-element branches).  G = 8 cuts the waits
+// 8x but holds 8 addresses; G = 1 for the register-capped callers.
+template <int G>
+__device__ __forceinline__ void load_factor_rows(const lds_float* tile, int r, bool fl,
+                                                 float (&a)[32]) {
+  if constexpr (G == 1) {
+#pragma unroll
+    for (int c = 0; c < 32; ++c) {
+      float t = tile[sw(r, c)];
+      asm volatile("" : "+v"(t));
+      a[c] = fl ? t : (c == r ? 1.0f : 0.0f);
+    }
+    return;
+  }
+#pragma unroll
+  for (int c0 = 0; c0 < 32; c0 += G) {
+#pragma unroll
+    for (int c = c0; c < c0 + G; ++c) a[c] = tile[sw(r, c)];
+#pragma unroll
+    for (int c = c0; c < c0 + G; ++c) asm volatile("" : "+v"(a[c]));
+  }
+#pragma unroll
+  for (int c = 0; c < 32; ++c) a[c] = fl ? a[c] : (c == r ? 1.0f : 0.0f);
+}
+
 __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
   const int r = lane & 31;
   const bool fl = lane < 32;
   float a[32];
-#pragma unroll
-  for (int c = 0; c < 32; ++c) {
-    float t = tile[sw(r, c)];  // both halves read (no divergent loads)
-    asm volatile("" : "+v"(t));  // keeps the load out of a per-element branch
-    a[c] = fl ? t : (c == r ? 1.0f : 0.0f);
-  }
+  load_factor_rows<1>(tile, r, fl, a);
   bool ok = true;
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
@@ -95,12 +118,7 @@ __device__ __noinline__ bool diag_factor_inv_blk(lds_float* tile, int lane) {
   const int r = lane & 31;
   const bool fl = lane < 32;
   float a[32];
-#pragma unroll
-  for (int c = 0; c < 32; ++c) {
-    float t = tile[sw(r, c)];
-    asm volatile("" : "+v"(t));
-    a[c] = fl ? t : (c == r ? 1.0f : 0.0f);
-  }
+  load_factor_rows<8>(tile, r, fl, a);
   bool ok = true;
   auto column = [&](int k, int m0) {  // column k from the terms m in [m0, k)
     float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;

@@ -107,6 +107,21 @@ __device__ __forceinline__ f32x16 mfma_x6(const bf16x8 (&a)[3], const bf16x8 (&b
   return c;
 }
 
+// The same six products ordered so that each one after the first needs one
+// more fragment than the one before it: the operand reads stagger behind
+// the MFMAs instead of all being waited on up front (c already holds the
+// running sum, so the order does not change the rounding).  Holds all six
+// fragments at once: for kernels with registers to spare (solve.hip).
+__device__ __forceinline__ f32x16 mfma_x6s(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 c) {
+  c = mfma_bf16(a[0], b[0], c);
+  c = mfma_bf16(a[0], b[1], c);
+  c = mfma_bf16(a[1], b[0], c);
+  c = mfma_bf16(a[0], b[2], c);
+  c = mfma_bf16(a[1], b[1], c);
+  c = mfma_bf16(a[2], b[0], c);
+  return c;
+}
+
 // Pieces of 8 consecutive-k values as three bf16x8 fragments.
 __device__ __forceinline__ void split3x8(const float (&x)[8], bf16x8 (&f)[3]) {
 #pragma unroll

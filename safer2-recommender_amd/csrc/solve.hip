@@ -423,7 +423,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
                 av[p] = st[bf_gran<Dp>(p, g, hi, aoff[m])];
                 bv[p] = st[bf_gran<Dp>(p, g, hi, boff[m])];
               }
-              acc[m] = mfma_x6(av, bv, acc[m]);
+              acc[m] = mfma_x6s(av, bv, acc[m]);
               if (m < NT / NW) split_slot(2 * m + g);
             }
           }
