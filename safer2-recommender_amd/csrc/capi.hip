@@ -855,9 +855,27 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
     HIP_TRY(c, launch_split_syrk(c->Dp, ap, s));
     ktimer_end(c, k, s);
   }
+  static const bool dprof = getenv("FRECSYS_DUAL_PROF") != nullptr;
+  static unsigned long long* d_prof = nullptr;
+  if (dprof && !d_prof) {
+    HIP_TRY(c, hipMalloc((void**)&d_prof, sizeof(unsigned long long) * 16));
+    HIP_TRY(c, hipMemset(d_prof, 0, sizeof(unsigned long long) * 16));
+  }
+  ap.prof = dprof ? d_prof : nullptr;
   const size_t k = ktimer_begin(c, pre + ".dspace", s);
   HIP_TRY(c, launch_solve(c->Dp, ap, s));
   ktimer_end(c, k, s);
+  if (dprof) {  // diagnostics: mean cycles per entity and phase
+    unsigned long long hp[16];
+    HIP_TRY(c, hipStreamSynchronize(s));
+    HIP_TRY(c, hipMemcpy(hp, d_prof, sizeof(hp), hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemset(d_prof, 0, sizeof(hp)));
+    const double n = (double)std::max<unsigned long long>(hp[4], 1);
+    fprintf(stderr, "[dspace-prof] %s n %llu mean h %.0f cycles/entity: setup %.0f syrk %.0f "
+            "epilogue %.0f chol %.0f | chain %.0f workers %.0f factored %.0f\n", pre.c_str(),
+            hp[4], hp[8] / n, hp[0] / n, hp[1] / n, hp[2] / n, hp[3] / n, hp[5] / n, hp[6] / n,
+            hp[7] / n);
+  }
   return FRECSYS_OK;
 }
 

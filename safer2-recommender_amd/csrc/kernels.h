@@ -46,6 +46,7 @@ struct SolveArgs {
   const float* other_weight;   // [rows of other side] nu
   unsigned long long* fail;    // atomicMin(entity + 1) on a non-SPD pivot
   int debug_skip;              // diagnostic ablation mask (0 in production)
+  unsigned long long* prof;    // diagnostics: per-phase cycle sums [16] (nullptr = off)
   // long-history split (tiled kernel only; nullptr / 0 = none)
   const int2* split;           // [n_split] per queue position: first slab, slab count
   int64_t n_split;

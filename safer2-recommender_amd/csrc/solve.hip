@@ -294,6 +294,15 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
   };
 
   if (tid == 0) flag[0] = 0;
+  // diagnostics (FRECSYS_DUAL_PROF): cycles per phase summed over entities
+  unsigned long long t_prev = (!PARTIAL && a.prof) ? clock64() : 0;
+  auto mark = [&](int ph) {
+    if (!PARTIAL && a.prof && tid == 0) {
+      const unsigned long long t = clock64();
+      atomicAdd(a.prof + ph, t - t_prev);
+      t_prev = t;
+    }
+  };
   if (tid < R) {  // ring prologue: the chunks the first iteration reads
 #pragma unroll
     for (int c = 0; c < (BF ? 3 : 2); ++c) {
@@ -359,6 +368,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     if (tid < Dp) bacc += sl[NT * 1024 + tid];
   }
   lds_barrier();
+  mark(0);
   if constexpr (BF) {
     // two chunks of row loads in flight: iteration c runs the MFMAs of
     // chunk c, stages chunk c+1 (registers xcur, loaded one iteration ago)
@@ -480,6 +490,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
       lds_barrier();
     }
   }
+  mark(1);
   if constexpr (BF) {
     // rhs: the two row groups' parts of each column (the stage is dead)
     if (bown && bg == 1) part[bc] = bpart;
@@ -528,6 +539,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     bvec[tid] = b;
   }
   lds_barrier();
+  mark(2);
 
   if (grad) {
     // ---- CVaR-MF: one gradient step with the full (stale-upper) matrix ----
@@ -549,12 +561,17 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
 
   // ---- blocked right-looking Cholesky with lookahead + back-solve ----
 #if FRECSYS_CHOL_DF
-  chol_solve_df<T, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
+  chol_solve_df<T, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip, a.prof);
 #else
   chol_solve_tiles<T, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
 #endif
+  mark(3);
   if (tid < Dp) a.out[e * Dp + tid] = xvec[tid];
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
+  if (a.prof && tid == 0) {
+    atomicAdd(a.prof + 4, 1ull);
+    atomicAdd(a.prof + 8, (unsigned long long)ntot);
+  }
 }
 
 // ---------------------------------------------------------------------
