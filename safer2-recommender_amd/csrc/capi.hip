@@ -872,9 +872,9 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
     HIP_TRY(c, hipMemset(d_prof, 0, sizeof(hp)));
     const double n = (double)std::max<unsigned long long>(hp[4], 1);
     fprintf(stderr, "[dspace-prof] %s n %llu mean h %.0f cycles/entity: setup %.0f syrk %.0f "
-            "epilogue %.0f chol %.0f | chain %.0f workers %.0f factored %.0f\n", pre.c_str(),
-            hp[4], hp[8] / n, hp[0] / n, hp[1] / n, hp[2] / n, hp[3] / n, hp[5] / n, hp[6] / n,
-            hp[7] / n);
+            "epilogue %.0f (rhs %.0f tiles %.0f) chol %.0f | chain %.0f workers %.0f factored %.0f\n",
+            pre.c_str(), hp[4], hp[8] / n, hp[0] / n, hp[1] / n, (hp[2] + hp[9] + hp[10]) / n,
+            hp[9] / n, hp[10] / n, hp[3] / n, hp[5] / n, hp[6] / n, hp[7] / n);
   }
   return FRECSYS_OK;
 }

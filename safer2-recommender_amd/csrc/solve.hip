@@ -30,6 +30,8 @@
 // solve by one lane (the reference's own tests run at dim 8).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "chol.h"
 #include "common.h"
 #include "kernels.h"
@@ -329,6 +331,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
                     a.lambda_is_reg);
   const bool grad = is_grad_kind(kind);
   const float gscale = kind == KIND_IALS ? a.w : (is_u_kind(kind) ? hf * a.w : a.w);
+  const float lam_d = kind == KIND_IALS ? lam : 0.0f;  // iALS: lambda rides in acc0
   f32x16 acc[MT];
   int aoff[MT], boff[MT];
   bool valid[MT];
@@ -346,9 +349,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int gi = 32 * I + acc_row(q, hi), gj = 32 * J + lo;
-        float v = gscale * a.G[gi * Dp + gj];
-        if (kind == KIND_IALS && gi == gj) v += lam;
-        acc[m][q] = v;
+        acc[m][q] = gscale * a.G[gi * Dp + gj] + (gi == gj ? lam_d : 0.0f);
       }
     }
   }
@@ -498,6 +499,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     if (tid < Dp) bacc += bpart + part[tid];
     lds_barrier();
   }
+  mark(9);
 
   if (PARTIAL) {
     float* sl = a.slabs + (size_t)slab0 * slab_floats;
@@ -514,25 +516,35 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
   }
 
   // ---- epilogue: finish A into the swizzled LDS tiles ----
+  // (the kind is dispatched once, outside the element loops: a per-element
+  // kind test compiled into ~7 scalar branches per element, 15K cycles)
   const float us = omega / hf;
+  auto write_tiles = [&](auto mode_c) {
+    constexpr int MODE = decltype(mode_c)::value;  // 0 iALS, 1 U kinds, 2 V kinds, 3 CVaR
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    if (valid[m]) {
-      const int I = (aoff[m] - lo) >> 5, J = (boff[m] - lo) >> 5;
-      float* tile = tiles + tidx(I, J) * 1024;
+    for (int m = 0; m < MT; ++m) {
+      if (valid[m]) {
+        const int I = (aoff[m] - lo) >> 5, J = (boff[m] - lo) >> 5;
+        float* tile = tiles + tidx(I, J) * 1024;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = acc_row(q, hi);
-        const bool dg = (32 * I + i) == (32 * J + lo);
-        float v = acc[m][q];
-        if (is_u_kind(kind) && !grad) v = v * us + (dg ? lam : 0.0f);
-        else if (vk && !grad) v = v + (dg ? lam : 0.0f);
-        else if (grad) v = assemble(kind, v, a.G[(32 * I + i) * Dp + 32 * J + lo], dg, a.w, lam,
-                                    hf, omega);
-        tile[sw(i, lo)] = v;
+        for (int q = 0; q < 16; ++q) {
+          const int i = acc_row(q, hi);
+          const bool dg = (32 * I + i) == (32 * J + lo);
+          float v = acc[m][q];
+          if constexpr (MODE == 1) v = v * us + (dg ? lam : 0.0f);
+          if constexpr (MODE == 2) v = v + (dg ? lam : 0.0f);
+          if constexpr (MODE == 3)
+            v = assemble(kind, v, a.G[(32 * I + i) * Dp + 32 * J + lo], dg, a.w, lam, hf, omega);
+          tile[sw(i, lo)] = v;
+        }
       }
     }
-  }
+  };
+  if (grad) write_tiles(std::integral_constant<int, 3>{});
+  else if (is_u_kind(kind)) write_tiles(std::integral_constant<int, 1>{});
+  else if (vk) write_tiles(std::integral_constant<int, 2>{});
+  else write_tiles(std::integral_constant<int, 0>{});
+  mark(10);
   if (tid < Dp) {
     float b = bacc;
     if (is_u_kind(kind)) b *= us;  // rhs *= weight / history_size
