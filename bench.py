@@ -169,8 +169,8 @@ def path_accounting(ctx, spec, ptrs, timers, K):
             unsplit, split = ds[ds <= 2 * split_rows], ds[ds > 2 * split_rows]
         f_fin = float(np.sum(unsplit) * d * (d + 1) + len(ds) * chol)
         ms, n = timers[name + ".dspace"]
-        if n:
-            fin_flops += f_fin * n / max(K, 1)
+        if n:  # per step: this side's d-space flops (one or two launches)
+            fin_flops += f_fin
             fin_ms += ms
             fin_n += n
         hsp = he[he <= dual_max] if dual_max > 0 else he[:0]
@@ -179,7 +179,8 @@ def path_accounting(ctx, spec, ptrs, timers, K):
         hs_ms, hs_n = timers[name + ".hspace"]
         paths[name] = {
             "dspace_entities": int(len(ds)), "dspace_ms": ms / max(K, 1),
-            "dspace_tflops": f_fin / (ms / max(n, 1) * 1e-3) / 1e12 if n else None,
+            "dspace_launches_per_step": n / max(K, 1),
+            "dspace_tflops": f_fin / (ms / max(K, 1) * 1e-3) / 1e12 if n else None,
             "split_rows_total": float(np.sum(split)),
             "split_ms": sp_ms / max(K, 1),
             "split_tflops": (float(np.sum(split)) * d * (d + 1) / (sp_ms / sp_n * 1e-3) / 1e12)
@@ -192,7 +193,7 @@ def path_accounting(ctx, spec, ptrs, timers, K):
             "rotate_ms": timers[name + ".rotate"][0] / max(K, 1),
         }
     avg_ms = fin_ms / max(fin_n, 1)
-    flops = fin_flops / max(fin_n / max(K, 1), 1)  # per launch
+    flops = fin_flops * max(K, 1) / max(fin_n, 1)  # per launch (mean over launches)
     return paths, avg_ms, flops
 
 
