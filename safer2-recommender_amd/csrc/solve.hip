@@ -519,7 +519,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
   // (the kind is dispatched once, outside the element loops: a per-element
   // kind test compiled into ~7 scalar branches per element, 15K cycles)
   const float us = omega / hf;
-  auto write_tiles = [&](auto mode_c) {
+  auto write_tiles = [&](auto mode_c) __attribute__((always_inline)) {
     constexpr int MODE = decltype(mode_c)::value;  // 0 iALS, 1 U kinds, 2 V kinds, 3 CVaR
 #pragma unroll
     for (int m = 0; m < MT; ++m) {

@@ -38,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "chol.h"
 #include "common.h"
@@ -159,7 +160,7 @@ __global__ void __launch_bounds__(512)
   }
   const int nchunks = (int)((nrow + W2R - 1) / W2R);
 
-  auto ring_load = [&](int c, int& id, float& sa, float& bw) {
+  auto ring_load = [&](int c, int& id, float& sa, float& bw) __attribute__((always_inline)) {
     const int64_t k = (int64_t)c * W2R + tid;
     id = -1;
     sa = 0.0f;
@@ -182,7 +183,7 @@ __global__ void __launch_bounds__(512)
       }
     }
   };
-  auto ring_store = [&](int c, int id, float sa, float bw) {
+  auto ring_store = [&](int c, int id, float sa, float bw) __attribute__((always_inline)) {
     const int sl = (c % W2RING) * W2R + tid;
     ring_id[sl] = id;
     ring_sa[sl] = sa;
@@ -196,7 +197,7 @@ __global__ void __launch_bounds__(512)
   const bool wside = MODE == 0 && !same && sc >= WB2;  // weighted B operand
   const bool bown = MODE == 1 && dgp;                  // diagonal pairs form b
   float xr[16];
-  auto load = [&](int c) {
+  auto load = [&](int c) __attribute__((always_inline)) {
     const int base = (c % W2RING) * W2R + 8 * hh0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -204,30 +205,34 @@ __global__ void __launch_bounds__(512)
       const int id = ring_id[base + r];
       // no select on the loaded value (rows past the end have sa = 0): the
       // loads stay in flight through the MFMAs of the current chunk
-      xr[r] = X[(int64_t)max(id, 0) * Dp + xcol];
+      xr[r] = FRECSYS_SKIP(a.debug_skip, 32) ? 0.0f : X[(int64_t)max(id, 0) * Dp + xcol];
     }
   };
   float bpart = 0.0f, btot = 0.0f;
-  auto stage_write = [&](int buf, int c) {
+  // staging math of one value (row r of the thread's column): scale, rhs
+  // part, 3-piece split into the fragment being assembled
+  auto stage_val = [&](int base, int r, bf16x8 (&f)[3], int j) __attribute__((always_inline)) {
+    const float sa = ring_sa[base + r];
+    float x = xr[r] * sa;
+    if (bown) bpart += ring_bw[base + r] * x;
+    if (wside) x *= ring_bw[base + r];
+    __bf16 ph, pm, pl;
+    split3(x, ph, pm, pl);
+    f[0][j] = ph;
+    f[1][j] = pm;
+    f[2][j] = pl;
+  };
+  // the whole chunk at once (prologue)
+  auto stage_write = [&](int buf, int c) __attribute__((always_inline)) {
     const int base = (c % W2RING) * W2R + 8 * hh0;
-    bf16x8* st = stage[buf];
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       if (same && hh > 0) break;
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int r = 8 * hh + j;
-        const float sa = ring_sa[base + r];
-        float x = xr[r] * sa;
-        if (bown) bpart += ring_bw[base + r] * x;
-        if (wside) x *= ring_bw[base + r];
-        v[j] = x;
-      }
       bf16x8 f[3];
-      split3x8(v, f);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) st[g2(p, hh0 + hh, sc)] = f[p];
+      for (int j = 0; j < 8; ++j) stage_val(base, 8 * hh + j, f, j);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) stage[buf][g2(p, hh0 + hh, sc)] = f[p];
     }
   };
 
@@ -237,17 +242,21 @@ __global__ void __launch_bounds__(512)
   // summing to 7: 9 tiles per SIMD on a diagonal pair, 16 on the others.
   constexpr int MT = 8;
   const int tI = wave < 4 ? wave : 11 - wave;
-  auto tv = [&](int m) { return !dgp || m <= tI; };  // wave-uniform
+  auto tv = [&](int m) __attribute__((always_inline)) {  // wave-uniform
+    return !dgp || m <= tI;
+  };
   const int boff = same ? 0 : WB2;  // B operand columns in the staged image
 
   float* const otile0 = MODE == 0 ? g.partials + unit * NT * 1024
                                   : ws + unit * ((int64_t)NT * 1024 + Dp);
-  auto otile = [&](int m) { return otile0 + (int64_t)tidx(8 * BI + tI, 8 * BJ + m) * 1024; };
+  auto otile = [&](int m) __attribute__((always_inline)) {
+    return otile0 + (int64_t)tidx(8 * BI + tI, 8 * BJ + m) * 1024;
+  };
   bool flushed = false;
   f32x16 acc[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = f32x16{0.f};
-  auto flush = [&]() {
+  auto flush = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       if (tv(m)) {  // wave-uniform
@@ -284,19 +293,26 @@ __global__ void __launch_bounds__(512)
   if (nchunks > 1) load(1);
   lds_barrier();
 
-  for (int c = 0; c < nchunks; ++c) {
-    const int buf = c & 1;
-    const bool more = c + 1 < nchunks;
-    const bool ring_more = (tid < W2R) && (c + 3 < nchunks);
-    int nid = -1;
-    float nsa = 0.f, nbw = 0.f;
-    if (ring_more) ring_load(c + 3, nid, nsa, nbw);
-    const bf16x8* st = stage[buf];
-    {
+  // chunk c: the MFMAs of its tiles, with chunk c+1's staging math (rows
+  // loaded one iteration ago) spread over the gaps between them -- a slice
+  // of NV/8 values after each tile, a granule group stored once complete --
+  // instead of a VALU phase of its own after the MFMAs
+  auto run = [&](auto same_c) __attribute__((always_inline)) {
+    constexpr bool SAME = decltype(same_c)::value;
+    constexpr int NV = SAME ? 8 : 16, PER = NV / MT;
+    for (int c = 0; c < nchunks; ++c) {
+      const int buf = c & 1;
+      const bool more = c + 1 < nchunks;
+      const bool ring_more = (tid < W2R) && (c + 3 < nchunks);
+      int nid = -1;
+      float nsa = 0.f, nbw = 0.f;
+      if (ring_more) ring_load(c + 3, nid, nsa, nbw);
+      const bf16x8* st = stage[buf];
+      bf16x8* sto = stage[buf ^ 1];
+      const int nbase = ((c + 1) % W2RING) * W2R + 8 * hh0;
       // A fragments of the wave's tile row, shared by its tiles; B fragments
-      // one tile ahead of their MFMAs (a deeper hoist of the LDS reads would
-      // not fit the 256 registers next to 8 accumulators)
-      bf16x8 af[3], bcur[3], bnxt[3];
+      // one tile ahead of their MFMAs
+      bf16x8 af[3], bcur[3], bnxt[3], fs[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         af[p] = st[g2(p, hi, 32 * tI + lo)];
@@ -309,21 +325,32 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
             for (int p = 0; p < 3; ++p) bnxt[p] = st[g2(p, hi, boff + 32 * (m + 1) + lo)];
           }
-          acc[m] = mfma_x6(af, bcur, acc[m]);
+          if (!FRECSYS_SKIP(a.debug_skip, 1)) acc[m] = mfma_x6(af, bcur, acc[m]);
 #pragma unroll
           for (int p = 0; p < 3; ++p) bcur[p] = bnxt[p];
         }
+        if (more) {  // block-uniform
+#pragma unroll
+          for (int u = 0; u < PER; ++u) {
+            const int r = m * PER + u;
+            stage_val(nbase, r, fs, r & 7);
+          }
+          if ((m * PER + PER) % 8 == 0) {
+            const int hh = (m * PER) >> 3;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) sto[g2(p, hh0 + hh, sc)] = fs[p];
+          }
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
+      if ((c + 1) % W2FLUSH == 0 && more) flush();  // block-uniform
+      if (more && c + 2 < nchunks) load(c + 2);
+      if (ring_more) ring_store(c + 3, nid, nsa, nbw);
+      lds_barrier();
     }
-    if ((c + 1) % W2FLUSH == 0 && more) flush();  // block-uniform
-    if (more) {
-      stage_write(buf ^ 1, c + 1);  // chunk c+1's rows (loaded last iteration)
-      if (c + 2 < nchunks) load(c + 2);
-    }
-    if (ring_more) ring_store(c + 3, nid, nsa, nbw);
-    lds_barrier();
-  }
+  };
+  if (same) run(std::true_type{});
+  else run(std::false_type{});
   if (flushed) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
@@ -358,32 +385,41 @@ __global__ void __launch_bounds__(512)
   const bool grad = is_grad_kind(kind);
   const float gscale = kind == KIND_IALS ? a.w : (is_u_kind(kind) ? hf * a.w : a.w);
   const float us = omega / hf;
+  // the kind is dispatched once, outside the element loops (a per-element
+  // kind test compiles into scalar branches per element)
+  auto finish = [&](auto mode_c) __attribute__((always_inline)) {
+    constexpr int FM = decltype(mode_c)::value;  // 0 iALS, 1 U kinds, 2 V kinds, 3 CVaR
 #pragma unroll
-  for (int m = 0; m < MT; ++m) {
-    if (tv(m)) {
-      float* t = otile(m);
-      const int I = 8 * BI + tI, J = 8 * BJ + m;
+    for (int m = 0; m < MT; ++m) {
+      if (tv(m)) {
+        float* t = otile(m);
+        const int I = 8 * BI + tI, J = 8 * BJ + m;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = acc_row(q, hi);
-        const int gi = 32 * I + i, gj = 32 * J + lo;
-        const bool dg = gi == gj;
-        float v = acc[m][q];
-        const float gv = a.G[(int64_t)gi * Dp + gj];
-        if (grad) {
-          v = assemble(kind, v, gv, dg, a.w, lam, hf, omega);
-        } else {
-          float g0 = gscale * gv;
-          if (kind == KIND_IALS && dg) g0 += lam;
-          v = g0 + v;  // accumulators started from the G part in the fp32 kernels
-          if (is_u_kind(kind)) v = v * us + (dg ? lam : 0.0f);
-          else if (vk) v = v + (dg ? lam : 0.0f);
+        for (int q = 0; q < 16; ++q) {
+          const int i = acc_row(q, hi);
+          const int gi = 32 * I + i, gj = 32 * J + lo;
+          const bool dg = gi == gj;
+          float v = acc[m][q];
+          const float gv = a.G[(int64_t)gi * Dp + gj];
+          if constexpr (FM == 3) {
+            v = assemble(kind, v, gv, dg, a.w, lam, hf, omega);
+          } else {
+            float g0 = gscale * gv;
+            if constexpr (FM == 0) g0 += dg ? lam : 0.0f;
+            v = g0 + v;  // accumulators started from the G part in the fp32 kernels
+            if constexpr (FM == 1) v = v * us + (dg ? lam : 0.0f);
+            if constexpr (FM == 2) v = v + (dg ? lam : 0.0f);
+          }
+          t[i * 32 + lo] = v;
         }
-        t[i * 32 + lo] = v;
       }
+      __builtin_amdgcn_sched_barrier(0);  // one tile's G loads live at a time
     }
-    __builtin_amdgcn_sched_barrier(0);  // one tile's G loads live at a time
-  }
+  };
+  if (grad) finish(std::integral_constant<int, 3>{});
+  else if (is_u_kind(kind)) finish(std::integral_constant<int, 1>{});
+  else if (vk) finish(std::integral_constant<int, 2>{});
+  else finish(std::integral_constant<int, 0>{});
   if (bown) {  // b of this diagonal block: the two row halves of each column
     if (tid >= WB2) bred[sc] = bpart;
     lds_barrier();
