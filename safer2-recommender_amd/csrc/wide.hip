@@ -125,8 +125,8 @@ __global__ void __launch_bounds__(512)
     wide_syrk2_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws,
                       int64_t n_units) {
   __shared__ __attribute__((aligned(16))) bf16x8 stage[2][W2GRAN];
-  __shared__ int ring_id[W2RING * W2R];
-  __shared__ float ring_sa[W2RING * W2R], ring_bw[W2RING * W2R];
+  __shared__ __attribute__((aligned(16))) int ring_id[W2RING * W2R];
+  __shared__ float2 ring_sb[W2RING * W2R];  // (row scale, rhs / B-side weight)
   __shared__ float bred[WB2];
   const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -186,8 +186,7 @@ __global__ void __launch_bounds__(512)
   auto ring_store = [&](int c, int id, float sa, float bw) __attribute__((always_inline)) {
     const int sl = (c % W2RING) * W2R + tid;
     ring_id[sl] = id;
-    ring_sa[sl] = sa;
-    ring_bw[sl] = bw;
+    ring_sb[sl] = make_float2(sa, bw);
   };
   const float* X = MODE == 0 ? g.X : a.X;
   // staging role: column sc of the staged image, rows 8*hh0 .. 8*hh0 + 8*nh - 1
@@ -199,23 +198,30 @@ __global__ void __launch_bounds__(512)
   float xr[16];
   auto load = [&](int c) __attribute__((always_inline)) {
     const int base = (c % W2RING) * W2R + 8 * hh0;
+    const int4* ids4 = reinterpret_cast<const int4*>(ring_id + base);  // base % 8 == 0
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (same && r >= 8) break;
-      const int id = ring_id[base + r];
-      // no select on the loaded value (rows past the end have sa = 0): the
-      // loads stay in flight through the MFMAs of the current chunk
-      xr[r] = FRECSYS_SKIP(a.debug_skip, 32) ? 0.0f : X[(int64_t)max(id, 0) * Dp + xcol];
+    for (int q = 0; q < 4; ++q) {
+      if (same && q >= 2) break;
+      const int4 i4 = ids4[q];
+      const int id[4] = {i4.x, i4.y, i4.z, i4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // no select on the loaded value (rows past the end have sa = 0): the
+        // loads stay in flight through the MFMAs of the current chunk.  32-bit
+        // element offsets (rows x Dp < 2^32, checked at launch)
+        const unsigned off = (unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)xcol;
+        xr[4 * q + j] = FRECSYS_SKIP(a.debug_skip, 32) ? 0.0f : X[off];
+      }
     }
   };
   float bpart = 0.0f, btot = 0.0f;
   // staging math of one value (row r of the thread's column): scale, rhs
   // part, 3-piece split into the fragment being assembled
   auto stage_val = [&](int base, int r, bf16x8 (&f)[3], int j) __attribute__((always_inline)) {
-    const float sa = ring_sa[base + r];
-    float x = xr[r] * sa;
-    if (bown) bpart += ring_bw[base + r] * x;
-    if (wside) x *= ring_bw[base + r];
+    const float2 sb = ring_sb[base + r];
+    float x = xr[r] * sb.x;
+    if (bown) bpart += sb.y * x;
+    if (wside) x *= sb.y;
     __bf16 ph, pm, pl;
     split3(x, ph, pm, pl);
     f[0][j] = ph;
@@ -834,6 +840,8 @@ int64_t wide_gram_num_blocks(int64_t n) {
 
 hipError_t launch_wide_gramian(int Dp, const GramArgs& g, hipStream_t s) {
   if (!wide_dim(Dp)) return hipErrorInvalidValue;
+  // 32-bit element offsets in the row gathers
+  if ((g.row0 + g.n) * (int64_t)Dp >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
   const int64_t rpb = wide_rows_per_block(g.n);
   const int64_t nblk = (g.n + rpb - 1) / rpb;
   if (nblk == 0) return hipMemsetAsync(g.G, 0, sizeof(float) * Dp * Dp, s);
@@ -849,6 +857,8 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                              hipStream_t s) {
   if (!wide_dim(Dp) || batch <= 0) return hipErrorInvalidValue;
   if (a.n_rows <= 0) return hipSuccess;
+  // 32-bit element offsets in the row gathers
+  if (a.n_other * (int64_t)Dp >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
     hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel,
