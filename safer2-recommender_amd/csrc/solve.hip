@@ -191,7 +191,8 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
         // no select on the loaded value: rows past the history have sa = 0
         // (split_bf), so the loads stay in flight through the MFMA phase
 #pragma unroll
-        for (int j = 0; j < 4; ++j) xr[4 * q + j] = a.X[(int64_t)max(id[j], 0) * Dp + bc];
+        for (int j = 0; j < 4; ++j)  // 32-bit element offsets (rows x Dp < 2^32, checked at launch)
+          xr[4 * q + j] = a.X[(unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)bc];
       }
     }
   };
@@ -769,6 +770,7 @@ int padded_dim(int dim) {
 
 hipError_t launch_solve(int Dp, const SolveArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
+  if (a.n_other * (int64_t)Dp >= ((int64_t)1 << 32)) return hipErrorInvalidValue;  // gathers
   switch (Dp) {
     case 8: return launch_small<8>(a, s);
     case 16: return launch_small<16>(a, s);
@@ -786,6 +788,7 @@ hipError_t launch_solve(int Dp, const SolveArgs& a, hipStream_t s) {
 
 hipError_t launch_split_syrk(int Dp, const SolveArgs& a, hipStream_t s) {
   if (a.n_work <= 0) return hipSuccess;
+  if (a.n_other * (int64_t)Dp >= ((int64_t)1 << 32)) return hipErrorInvalidValue;  // gathers
   switch (Dp) {
     case 32: return launch_tiled<1, true>(a, s);
     case 64: return launch_tiled<2, true>(a, s);
