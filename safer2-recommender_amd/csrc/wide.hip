@@ -13,13 +13,13 @@
 //                        LDS as bf16 pieces, 16 per chunk, one chunk ahead),
 //                        two-level accumulation, the G part of A added in the
 //                        epilogue; the diagonal pairs also form b.
-//   wide_chol_kernel     one workgroup (8 waves) per entity: right-looking
-//                        blocked Cholesky over the workspace tiles -- the
-//                        diagonal tile factored and inverted in LDS
-//                        (diag_factor_inv), the panel column TRSM'd by MFMA
-//                        into LDS (it is read by every trailing update of the
-//                        step), trailing tiles updated in place, y = L^-1 b
-//                        riding along, then x = L^-T y.
+//   wide_chol_kernel     one workgroup (8 waves) per entity: left-looking
+//                        blocked Cholesky over the workspace tiles -- row p
+//                        of L staged in LDS, the diagonal tile updated,
+//                        factored and inverted in LDS (diag_factor_inv), the
+//                        panel tiles summed from the streamed L tiles and
+//                        finished by MFMA with L_pp^-T, y = L^-1 b riding
+//                        along, then x = L^-T y.
 //   wide_grad_kernel     CVaR-MF's gradient step with the stale upper
 //                        triangle (cvar_mf.h:133, 179).
 //
@@ -43,6 +43,13 @@
 #include "chol.h"
 #include "common.h"
 #include "kernels.h"
+
+// waves per SIMD wide_chol_kernel<16> is compiled for (4: two workgroups per
+// CU, 128 registers, 30.5 ms at MSD; 2: one workgroup, 256 registers,
+// 32.1 ms); at Dp = 1024 row p of L alone takes 128 KB of LDS: 2.
+#ifndef FRECSYS_WIDE_CHOL_WPE
+#define FRECSYS_WIDE_CHOL_WPE 4
+#endif
 
 namespace frecsys_hip {
 
@@ -453,20 +460,42 @@ __global__ void __launch_bounds__(256)
 }
 
 // One workgroup (8 waves) per entity of the batch: A x = b with A's lower
-// tiles in the entity's workspace slot (row-major 32x32 tiles, tidx order).
-// LDS: the diagonal slot, the panel column (swizzled), b / y, x, partials.
+// tiles in the entity's workspace slot (row-major 32x32 tiles, tidx order),
+// left-looking blocked Cholesky.  Panel p
+//   A  row p of L (tiles (p, q), q < p, final) into LDS, swizzled;
+//   B  wave 0: D = A_pp - sum_q L_pq L_pq^T, factored + inverted in LDS
+//      (diag_factor_inv) and L_pp^-1 stored back for the back substitution;
+//      wave 1 first: r_p = b_p - sum_q L_pq y_q;
+//      waves 1..7, tiles I > p round-robin: C_I = (A_Ip - sum_q L_Iq L_pq^T)^T
+//      in accumulator registers, L_Iq streamed from the workspace straight
+//      into MFMA operand registers (k-order of that product: lane half hi
+//      takes k = 16 hi + s, i.e. 4 float4 loads of its row);
+//   C  waves 1..7: L_Ip = C_I^T L_pp^-T, C_I used as the MFMA A operand as it
+//      sits in the accumulators (k = acc_row(s, hi)); wave 0: y_p = L_pp^-1 r_p.
+// Each tile of A is read once and each tile of L written once; L tiles are
+// re-read by later panels: ~T^3/6 tile reads + T^2/2 writes per entity
+// against ~T^3/3 reads and T^3/3 writes of a right-looking update sweep
+// (round 2's kernel: MSD 174 GB of workspace traffic per epoch, 37 ms; this
+// one 30.5 ms).  Compiled for two workgroups per CU (128 registers).
+template <int T>
 __global__ void __launch_bounds__(512)
-    wide_chol_kernel(SolveArgs a, int Dp, int64_t pos0, float* ws) {
+    __attribute__((amdgpu_waves_per_eu(T == 16 ? FRECSYS_WIDE_CHOL_WPE : 2, 8)))
+    wide_chol_kernel(SolveArgs a, int64_t pos0, float* ws) {
+  constexpr int Dp = 32 * T, NT = T * (T + 1) / 2, NW = 8;
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int NW = 8;
-  const int T = Dp >> 5, NT = T * (T + 1) / 2;
-  float* dslot = smem;
-  float* pan = smem + 1024;
-  float* bvec = pan + T * 1024;
-  float* xvec = bvec + Dp;
-  float* part = xvec + Dp;
-  float* ytmp = part + NW * 32;
-  int* flag = reinterpret_cast<int*>(ytmp + 32);
+  // LDS tiles of row p of L and of L_pp^-1 are row-major with a 33-float
+  // row stride (lane lo reads row lo at immediate offsets, conflict-free);
+  // the diagonal factor works on its own swizzled tile
+  constexpr int LP = 33 * 32;
+  float* rowL = smem;                   // [T-1][LP], row p of L
+  float* dpad = rowL + (T - 1) * LP;    // L_pp^-1
+  float* dinv = dpad + LP;              // swizzled factor tile
+  float* yv = dinv + 1024;              // b, then y
+  float* xv = yv + Dp;
+  float* rv = xv + Dp;                  // r_p
+  float* part = rv + 32;                // NW x 32 back-substitution partials
+  int* flag = reinterpret_cast<int*>(part + NW * 32);
   const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const QueueRec rec = a.order[pos0 + blockIdx.x];
@@ -474,126 +503,151 @@ __global__ void __launch_bounds__(512)
   if (rec.h == 0) return;
   float* slot = ws + (int64_t)blockIdx.x * ((int64_t)NT * 1024 + Dp);
   auto gtile = [&](int I, int J) { return slot + (int64_t)tidx(I, J) * 1024; };
-  for (int i = tid; i < Dp; i += 512) bvec[i] = slot[(int64_t)NT * 1024 + i];
+  for (int i = tid; i < Dp; i += 512) yv[i] = slot[(int64_t)NT * 1024 + i];
   if (tid == 0) flag[0] = 0;
   __syncthreads();
 
+  // C_I = (A_Ip - sum_{q<p} L_Iq L_pq^T)^T in accumulator registers: A_Ip^T
+  // as its rows, L_Iq streamed from the workspace into operand registers
+  // (k = 16 hi + s), the next tile's loads in flight under each product
+  auto panel_sum = [&](int I, int p) __attribute__((always_inline)) {
+    const float* Aip = gtile(I, p) + lo * 32 + 4 * hi;
+    f32x16 c;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // row lo, columns acc_row(4g + j, hi)
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(Aip + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[4 * g + j] = v[j];
+    }
+    f32x4v cur[4], nxt[4];
+    if (p > 0) {
+      const f32x4v* L0 = reinterpret_cast<const f32x4v*>(gtile(I, 0) + lo * 32 + 16 * hi);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = L0[j];
+    }
+#pragma unroll 1
+    for (int q = 0; q < p; ++q) {
+      if (q + 1 < p) {
+        const f32x4v* Ln = reinterpret_cast<const f32x4v*>(gtile(I, q + 1) + lo * 32 + 16 * hi);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nxt[j] = Ln[j];
+      }
+      const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+    }
+    return c;
+  };
+
 #pragma unroll 1
   for (int p = 0; p < T; ++p) {
-    // diagonal tile: L_pp^-1 into dslot (and back to the workspace for the
-    // back substitution), y_p = L_pp^-1 b_p
+    // ---- A: row p of L ----
+    for (int i = tid; i < p * 256; i += 512) {
+      const int q = i >> 8, r = (i >> 3) & 31, c = (i & 7) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(gtile(p, q) + r * 32 + c);
+      float* t = rowL + q * LP + r * 33 + c;
+      t[0] = v.x;
+      t[1] = v.y;
+      t[2] = v.z;
+      t[3] = v.w;
+    }
+    __syncthreads();
+    // ---- B ----
+    f32x16 acc0;
     if (wave == 0) {
-      const float* A = gtile(p, p);
+      const float* App = gtile(p, p);
+      f32x16 d;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) d[q] = App[acc_row(q, hi) * 32 + lo];
+#pragma unroll 1
+      for (int q = 0; q < p; ++q) {  // d -= L_pq L_pq^T (k = 16 hi + s)
+        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
+      }
+      // opaque zero: the swizzled addresses are formed here, not hoisted out
+      // of the panel loop into registers for its whole length
+      int z;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dinv[sw(acc_row(q, hi), lo) + z] = d[q];
+      wave_lds_sync();
+      if (!diag_factor_inv(dinv, lane) && lane == 0) flag[0] = 1;
+      wave_lds_sync();
+      float* Aw = gtile(p, p);  // L_pp^-1 for the back substitution, and its padded copy
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int idx = lane + 64 * i;
-        dslot[sw(idx >> 5, idx & 31)] = A[idx];
+        const int r = 2 * i + hi;
+        const float v = dinv[sw(r, lo) + z];
+        Aw[r * 32 + lo] = v;
+        dpad[r * 33 + lo] = v;
       }
-      wave_lds_sync();
-      if (!diag_factor_inv(dslot, lane) && lane == 0) flag[0] = 1;
-      wave_lds_sync();
+    } else {
+      if (wave == 1) {
+        float r = 0.0f;
+#pragma unroll 1
+        for (int q = 0; q < p; ++q) {  // row lo of L_pq . y_q, k halves by hi
+          const float* L = rowL + q * LP + lo * 33 + 16 * hi;
+          const float* y = yv + 32 * q + 16 * hi;
+#pragma unroll
+          for (int k2 = 0; k2 < 16; ++k2) r += L[k2] * y[k2];
+        }
+        r += __shfl_xor(r, 32);
+        if (hi == 0) rv[lo] = yv[32 * p + lo] - r;
+      }
+      if (p + wave < T) acc0 = panel_sum(p + wave, p);  // first panel tile
+    }
+    __syncthreads();
+    // ---- C ----
+    if (wave == 0) {
       float y = 0.0f;
-#pragma unroll 8
-      for (int k = 0; k < 32; ++k) y += dslot[sw(lo, k)] * bvec[32 * p + k];
-      wave_lds_sync();
-      if (hi == 0) bvec[32 * p + lo] = y;
-      float* Aw = gtile(p, p);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int idx = lane + 64 * i;
-        Aw[idx] = dslot[sw(idx >> 5, idx & 31)];
-      }
-    }
-    __syncthreads();
-    // panel: L_Ip = A_Ip (L_pp^-1)^T into LDS (and the workspace); b_I -= L_Ip y_p
+      for (int k2 = 0; k2 < 16; ++k2) y += dpad[lo * 33 + 16 * hi + k2] * rv[16 * hi + k2];
+      y += __shfl_xor(y, 32);
+      if (hi == 0) yv[32 * p + lo] = y;
+    } else {
+      // first tile from its B-phase sum, the rest sum-then-finish (L_pp^-1 is ready)
 #pragma unroll 1
-    for (int I = p + 1 + wave; I < T; I += NW) {
-      float* Pl = pan + I * 1024;
-      float* Ag = gtile(I, p);
+      for (int I = p + wave; I < T; I += NW - 1) {
+        const f32x16 cI = I == p + wave ? acc0 : panel_sum(I, p);
+        f32x16 l = f32x16{0.f};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int idx = lane + 64 * i;
-        Pl[sw(idx >> 5, idx & 31)] = Ag[idx];
+        for (int s2 = 0; s2 < 16; ++s2) l = mfma32(cI[s2], dpad[lo * 33 + acc_row(s2, hi)], l);
+        float* Lw = gtile(I, p);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) Lw[acc_row(q, hi) * 32 + lo] = l[q];
       }
-      wave_lds_sync();
-      const f32x16 u = tile_pqT(Pl, dslot, lo, hi);
-      wave_lds_sync();
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int r = acc_row(q, hi);
-        Pl[sw(r, lo)] = u[q];
-        Ag[r * 32 + lo] = u[q];
-      }
-      wave_lds_sync();
-      if (hi == 0) {
-        float s = 0.0f;
-#pragma unroll 8
-        for (int k = 0; k < 32; ++k) s += Pl[sw(lo, k)] * bvec[32 * p + k];
-        bvec[32 * I + lo] -= s;
-      }
-    }
-    __syncthreads();
-    // trailing update A_IJ -= L_Ip L_Jp^T, p < J <= I
-    // (software-pipelined: the next tile's loads are in flight under this
-    // tile's MFMAs)
-    const int m = T - 1 - p, ntr = m * (m + 1) / 2;
-    auto tile_ij = [&](int tt, int& I, int& J) {
-      int Ir = 0;
-      while ((Ir + 1) * (Ir + 2) / 2 <= tt) ++Ir;
-      I = p + 1 + Ir;
-      J = p + 1 + tt - Ir * (Ir + 1) / 2;
-    };
-    int In = 0, Jn = 0;
-    f32x16 vn;
-    if (wave < ntr) {
-      tile_ij(wave, In, Jn);
-      const float* An = gtile(In, Jn);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) vn[q] = An[acc_row(q, hi) * 32 + lo];
-    }
-#pragma unroll 1
-    for (int tt = wave; tt < ntr; tt += NW) {
-      const int I = In, J = Jn;
-      const f32x16 v = vn;
-      if (tt + NW < ntr) {
-        tile_ij(tt + NW, In, Jn);
-        const float* An = gtile(In, Jn);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) vn[q] = An[acc_row(q, hi) * 32 + lo];
-      }
-      const f32x16 u = tile_pqT(pan + I * 1024, pan + J * 1024, lo, hi);
-      float* Ag = gtile(I, J);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) Ag[acc_row(q, hi) * 32 + lo] = v[q] - u[q];
     }
     __syncthreads();
   }
 
-  // back substitution x_p = L_pp^-T (y_p - sum_{q>p} L_qp^T x_q)
+  // ---- back substitution x_p = L_pp^-T (y_p - sum_{q>p} L_qp^T x_q) ----
 #pragma unroll 1
   for (int p = T - 1; p >= 0; --p) {
     float pr = 0.0f;
     for (int q = p + 1 + wave; q < T; q += NW) {
       const float* L = gtile(q, p);
 #pragma unroll 4
-      for (int mm = 16 * hi; mm < 16 * hi + 16; ++mm) pr += L[mm * 32 + lo] * xvec[32 * q + mm];
+      for (int mm = 16 * hi; mm < 16 * hi + 16; ++mm) pr += L[mm * 32 + lo] * xv[32 * q + mm];
     }
     pr += __shfl_xor(pr, 32);
     if (hi == 0) part[wave * 32 + lo] = pr;
     __syncthreads();
     if (wave == 0) {
-      float r = bvec[32 * p + lo];
+      float r = yv[32 * p + lo];
 #pragma unroll
       for (int w = 0; w < NW; ++w) r -= part[w * 32 + lo];
       const float* Li = gtile(p, p);
       float x = 0.0f;
 #pragma unroll 8
       for (int i = 0; i < 32; ++i) x += Li[i * 32 + lo] * rdlane(r, i);
-      if (hi == 0) xvec[32 * p + lo] = x;
+      if (hi == 0) xv[32 * p + lo] = x;
     }
     __syncthreads();
   }
-  for (int i = tid; i < Dp; i += 512) a.out[e * Dp + i] = xvec[i];
+  for (int i = tid; i < Dp; i += 512) a.out[e * Dp + i] = xv[i];
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
@@ -821,8 +875,9 @@ unsigned xcd_grid(int64_t n_units, int P) { return (unsigned)(((n_units + 7) / 8
 
 size_t wide_chol_lds_bytes(int Dp) {
   const int T = Dp >> 5;
-  return sizeof(float) * ((size_t)1024 + (size_t)T * 1024 + 2 * Dp + 8 * 32 + 32 + 4);
+  return sizeof(float) * ((size_t)T * 33 * 32 + 1024 + 2 * Dp + 32 + 8 * 32 + 4);
 }
+
 
 }  // namespace
 
@@ -861,9 +916,13 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
   if (a.n_other * (int64_t)Dp >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)wide_chol_lds_bytes(1024));
+    hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel<16>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)wide_chol_lds_bytes(512));
+    if (err == hipSuccess)
+      err = hipFuncSetAttribute((const void*)wide_chol_kernel<32>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)wide_chol_lds_bytes(1024));
     if (err != hipSuccess) return err;
     attr = true;
   }
@@ -875,9 +934,12 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                        a, g, Dp, (int64_t)0, s0, ws, nb);
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
+    else if (Dp == 512)
+      hipLaunchKernelGGL(wide_chol_kernel<16>, dim3((unsigned)nb), dim3(512),
+                         wide_chol_lds_bytes(Dp), s, a, s0, ws);
     else
-      hipLaunchKernelGGL(wide_chol_kernel, dim3((unsigned)nb), dim3(512),
-                         wide_chol_lds_bytes(Dp), s, a, Dp, s0, ws);
+      hipLaunchKernelGGL(wide_chol_kernel<32>, dim3((unsigned)nb), dim3(512),
+                         wide_chol_lds_bytes(Dp), s, a, s0, ws);
   }
   return hipGetLastError();
 }
