@@ -8,7 +8,11 @@
 // ComputeUserLoss; then xi by smoothed-quantile Newton with Armijo.
 #pragma once
 
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <future>
 #include <random>
 #include <tuple>
 #include <vector>
@@ -30,6 +34,12 @@ inline float gaussian_kernel_cdf(const float u, const float h) {
 }
 inline float gaussian_loss(const float u, const float h, const float alpha) {
   const float ell = h * gaussian_kernel(u, h) + (u / h) * (1 - 2 * gaussian_kernel_cdf(-u, h));
+  return (float)((double)((h / 2) * ell) + ((double)(1 - alpha) - 0.5) * (double)u);
+}
+// gaussian_loss with gaussian_kernel(u, h) = k and gaussian_kernel_cdf(-u, h) = c given
+inline float gaussian_loss_from(const float u, const float h, const float alpha, const float k,
+                                const float c) {
+  const float ell = h * k + (u / h) * (1 - 2 * c);
   return (float)((double)((h / 2) * ell) + ((double)(1 - alpha) - 0.5) * (double)u);
 }
 inline float epanechnikov_kernel(const float u, const float h) {
@@ -72,7 +82,7 @@ struct Smoother {
     tc.resize((size_t)n);
     tk.resize((size_t)n);
     tl.resize((size_t)n);
-    ThreadPool::Get().ParallelFor(n, 2048, [&](int64_t lo, int64_t hi) {
+    ThreadPool::Get().ParallelFor(n, 512, [&](int64_t lo, int64_t hi) {
       for (int64_t i = lo; i < hi; ++i) {
         const float u = loss[i] - xi;
         if (epan) {
@@ -80,9 +90,15 @@ struct Smoother {
           tk[i] = epanechnikov_kernel(-u, bandwidth);
           tl[i] = epanechnikov_loss(u, bandwidth, alpha);
         } else {
-          tc[i] = gaussian_kernel_cdf(-u, bandwidth);
-          tk[i] = gaussian_kernel(-u, bandwidth);
-          tl[i] = gaussian_loss(u, bandwidth, alpha);
+          // gaussian_loss(u) re-evaluates gaussian_kernel(u) -- equal bit for
+          // bit to gaussian_kernel(-u): (-u)/h = -(u/h) exactly and the
+          // kernel squares it -- and gaussian_kernel_cdf(-u): each is
+          // evaluated once here (one erfc and one exp per sample)
+          const float c = gaussian_kernel_cdf(-u, bandwidth);
+          const float k = gaussian_kernel(-u, bandwidth);
+          tc[i] = c;
+          tk[i] = k;
+          tl[i] = gaussian_loss_from(u, bandwidth, alpha, k, c);
         }
       }
     });
@@ -191,15 +207,31 @@ class SAFER2Recommender : public detail::DeviceModel {
   }
 
   void Train(const Dataset& data) override {
+    // FRECSYS_HOST_PROF (diagnostics): wall ms of each Train() phase on stderr
+    static const bool hprof = getenv("FRECSYS_HOST_PROF") != nullptr;
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    auto t0 = now();
+    StartSnrDraws();  // the sample indices of this epoch's ComputeXi, drawn during the solves
     dev_->LoadTraining(data);
     PrintLosses(data);
+    auto t1 = now();
+    double tw = 0, tu = 0, tv = 0, tl = 0;
     for (int t = 0; t < pd_iterations_; ++t) {
+      auto a = now();
       ComputeUserWeights(data);                                   // safer2.h:272-273
+      auto b = now();
       frecsys_solve_params pu = u_params(true);
       dev_->Solve(DeviceContext::USER, pu);                       // safer2.h:277-285
+      auto c = now();
       StepV(data);                                                // safer2.h:288-290
+      auto d = now();
       dev_->Gramian(DeviceContext::ITEM);                         // safer2.h:294-295
       dev_->UserLoss(DeviceContext::USER, unobserved_weight_, true, user_loss_.data());
+      tw += ms(a, b);
+      tu += ms(b, c);
+      tv += ms(c, d);
+      tl += ms(d, now());
       VectorXf wl(num_users_);
       for (int64_t u = 0; u < num_users_; ++u) wl[u] = dual_weight_[u] * user_loss_[u];
       LOG(INFO) << "Weighted Loss: " << wl.mean();                // safer2.h:300-301
@@ -211,13 +243,19 @@ class SAFER2Recommender : public detail::DeviceModel {
       if (print_residualstats_)
         LOG(INFO) << format("U residual: {0}, V residual: {1}, z residual: {2}", 0.0f, 0.0f, 0.0f);
     }
+    auto x0 = now();
     const float xi = ComputeXi(user_loss_, prev_xi_, xi_iterations_);  // safer2.h:331-333
     LOG(INFO) << "Xi:" << xi;
     prev_xi_ = xi;
+    if (hprof)
+      fprintf(stderr, "[host-prof] train %.2f ms: load+print %.2f weights %.2f solveU %.2f "
+              "stepV %.2f gram+loss %.2f xi %.2f\n", ms(t0, now()), ms(t0, t1), tw, tu, tv, tl,
+              ms(x0, now()));
   }
 
   // Initialize (safer2.h:819-838).
   void Initialize(const Dataset& data) {
+    StartSnrDraws();
     dev_->LoadTraining(data);
     dev_->Gramian(DeviceContext::ITEM);
     dev_->UserLoss(DeviceContext::USER, unobserved_weight_, true, user_loss_.data());
@@ -233,20 +271,46 @@ class SAFER2Recommender : public detail::DeviceModel {
   float ComputeXi(const VectorXf& user_loss, const float prev_xi, const int nr_iterations) {
     float xi = prev_xi;
     const int64_t n = user_loss.size();
+    const int ns = (int)(n * sampling_ratio_);
+    std::vector<int> idx;
+    if (snr_draws_.valid()) {  // drawn ahead from snr_rng_, the same sequence (joined
+      idx = snr_draws_.get();  // before snr_rng_ is touched here)
+      if (idx.size() != (size_t)nr_iterations * ns) idx.clear();
+    }
     for (int t = 0; t < nr_iterations; ++t) {
       float d;
       if (!use_snr_) {
         d = smoother_.Direction(xi, user_loss.data(), n);
       } else {
-        std::uniform_int_distribution<int> uni(0, (int)n - 1);
-        const int ns = (int)(n * sampling_ratio_);
         std::vector<float> sample((size_t)ns);
-        for (int j = 0; j < ns; j++) sample[j] = user_loss[uni(snr_rng_)];
+        if (!idx.empty()) {
+          for (int j = 0; j < ns; j++) sample[j] = user_loss[idx[(size_t)t * ns + j]];
+        } else {
+          std::uniform_int_distribution<int> uni(0, (int)n - 1);
+          for (int j = 0; j < ns; j++) sample[j] = user_loss[uni(snr_rng_)];
+        }
         d = smoother_.Direction(xi, sample.data(), ns);
       }
       xi = xi + d;
     }
     return xi;
+  }
+
+  // The SNR sample indices depend only on snr_rng_ (not on the losses): the
+  // next ComputeXi's are drawn on a helper thread while this thread drives
+  // the GPU half-steps (uniform_int_distribution keeps no state between
+  // draws, so one distribution object yields the reference's sequence).
+  void StartSnrDraws() {
+    if (!use_snr_ || xi_iterations_ <= 0 || snr_draws_.valid()) return;
+    const int64_t n = num_users_;
+    const int ns = (int)(n * sampling_ratio_);
+    const int iters = xi_iterations_;
+    snr_draws_ = std::async(std::launch::async, [this, n, ns, iters] {
+      std::vector<int> idx((size_t)iters * ns);
+      std::uniform_int_distribution<int> uni(0, (int)n - 1);
+      for (auto& v : idx) v = uni(snr_rng_);
+      return idx;
+    });
   }
 
   float GetMeanWeight() const { return dual_weight_.mean(); }  // safer2.h:815-817
@@ -306,6 +370,7 @@ class SAFER2Recommender : public detail::DeviceModel {
   int pd_iterations_;
   uint64_t weight_epoch_ = 0;
   std::mt19937 snr_rng_;
+  std::future<std::vector<int>> snr_draws_;  // ComputeXi's next sample indices
 };
 
 }  // namespace frecsys
