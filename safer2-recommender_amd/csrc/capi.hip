@@ -131,6 +131,27 @@ struct frecsys_ctx {
   size_t cap_slabs = 0;
   std::vector<int32_t> order_h[3];       // history lengths in queue order
   int dual_on = 1;
+  // Content versions (every write of a side's embeddings or Gramian takes a
+  // fresh number): a Gramian recomputed from unchanged embeddings is reused
+  // (the computation is deterministic, the result would be identical), and
+  // a basis / rotated copy is rebuilt only when its inputs changed.  When a
+  // Gramian is formed for a side whose consumer last took the history-space
+  // path, its basis is built right away on stream5 (e.g. during the user
+  // loss and the host's xi / omega math between epochs) instead of on the
+  // next solve's critical path.
+  uint64_t ver_counter = 0;
+  uint64_t emb_ver[3] = {0, 0, 0};
+  uint64_t gram_ver[2] = {0, 0};
+  uint64_t gram_src[2] = {0, 0};    // emb_ver the Gramian was formed from (0: not reusable)
+  uint64_t basis_gram[2] = {0, 0};  // gram_ver the basis (T, Q, Q pieces) belongs to
+  uint64_t xrot_emb[2] = {0, 0};    // emb_ver of the rotated copy (0: stale / snapshot)
+  uint64_t xrot_gram[2] = {0, 0};   // ... and the basis it was rotated into
+  bool dual_used[3] = {false, false, false};  // the side's last solve took history space
+  int eager_on = 1;                 // FRECSYS_EAGER=0: no early basis builds (A/B)
+  hipStream_t stream5 = nullptr;
+  hipEvent_t ev_pre5 = nullptr;
+  hipEvent_t ev_eager[2] = {nullptr, nullptr};
+  bool eager_pending[2] = {false, false};
   int dual_max_h = 256;  // longest h_eff on the history-space path (set per Dp at create)
   int dual_serial = 0;  // FRECSYS_DUAL_SERIAL=1: no stream overlap (profiling)
   int debug_skip = 0;   // FRECSYS_DEBUG_SKIP ablation mask (-DFRECSYS_ABLATION builds only)
@@ -296,8 +317,21 @@ int plan_split(frecsys_ctx* c, const std::vector<int32_t>& hs, int64_t n,
   return FRECSYS_OK;
 }
 
+// Stream s waits (on the device) for the early basis builds still running
+// on stream5 (mask bit per side).
+int join_eager(frecsys_ctx* c, int mask, hipStream_t s) {
+  for (int t = 0; t < 2; ++t)
+    if ((mask >> t & 1) && c->eager_pending[t]) {
+      HIP_TRY(c, hipStreamWaitEvent(s, c->ev_eager[t], 0));
+      c->eager_pending[t] = false;
+    }
+  return FRECSYS_OK;
+}
+void emb_written(frecsys_ctx* c, int side) { c->emb_ver[side] = ++c->ver_counter; }
+
 // Basis of the other side's Gramian, G = Q T Q^T, and the other side
-// rotated into it (X Q): the inputs of the history-space solve.
+// rotated into it (X Q): the inputs of the history-space solve.  Rebuilt
+// only when the Gramian (basis) or the rows (rotation) changed since.
 int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
   const int Dp = c->Dp;
   size_t cap = 0;
@@ -311,9 +345,27 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
     rc = ensure(c, &c->refl[other], &cap, (size_t)Dp * Dp + Dp);
     if (rc) return rc;
   }
+  const bool need_basis = c->basis_gram[other] == 0 || c->basis_gram[other] != c->gram_ver[other];
+  const uint64_t xkey = X == c->emb[other] ? c->emb_ver[other] : 0;
+  const bool need_rot = need_basis || xkey == 0 || c->xrot_emb[other] != xkey ||
+                        c->xrot_gram[other] != c->gram_ver[other];
+  if (s != c->stream5) {
+    // an early build of this basis (or one sharing tri_work) may still run
+    int rc = join_eager(c, 3, s);
+    if (rc) return rc;
+  }
+  if (!need_rot) return FRECSYS_OK;
   int rc = ensure(c, &c->xrot[other], &c->cap_xrot[other],
                   (size_t)std::max<int64_t>(c->n[other], 1) * Dp);
   if (rc) return rc;
+  c->xrot_emb[other] = xkey;
+  c->xrot_gram[other] = c->gram_ver[other];
+  if (!need_basis) {
+    HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp,
+                             s));
+    return FRECSYS_OK;
+  }
+  c->basis_gram[other] = c->gram_ver[other];
   float* tau = c->refl[other] + (size_t)Dp * Dp;
   if (wide_dim(Dp)) {
     rc = ensure(c, &c->tri_work, &c->cap_tri_work, wide_tridiag_work_floats(Dp));
@@ -327,6 +379,26 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
     HIP_TRY(c, launch_split_basis(c->q[other], Dp, t, c->qsplit[other][t], s));
   }
   HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp, s));
+  return FRECSYS_OK;
+}
+
+// A Gramian of side g was just formed on c->stream: build its basis on
+// stream5 now if the side that consumes it took the history-space path last
+// time and will want it again.
+int maybe_start_eager(frecsys_ctx* c, int g) {
+  const int consumer = 1 - g;
+  if (!c->eager_on || c->dual_serial || !c->dual_on || c->Dp < 64 || c->dual_max_h <= 0 ||
+      !c->dual_used[consumer] || c->eager_pending[g])
+    return FRECSYS_OK;
+  if (c->basis_gram[g] == c->gram_ver[g] && c->xrot_emb[g] == c->emb_ver[g] &&
+      c->xrot_gram[g] == c->gram_ver[g])
+    return FRECSYS_OK;  // already current
+  HIP_TRY(c, hipEventRecord(c->ev_pre5, c->stream));
+  HIP_TRY(c, hipStreamWaitEvent(c->stream5, c->ev_pre5, 0));
+  int rc = prepare_basis(c, g, c->emb[g], c->stream5);
+  if (rc) return rc;
+  HIP_TRY(c, hipEventRecord(c->ev_eager[g], c->stream5));
+  c->eager_pending[g] = true;
   return FRECSYS_OK;
 }
 
@@ -520,7 +592,13 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
       hipEventCreateWithFlags(&c->ev_fork3, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join3, hipEventDisableTiming) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed (stream2/3)"));
+  if (hipStreamCreateWithFlags(&c->stream5, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pre5, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_eager[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_eager[1], hipEventDisableTiming) != hipSuccess)
+    return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed (stream5)"));
   if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
+  if (const char* v = getenv("FRECSYS_EAGER")) c->eager_on = atoi(v);
   // d-space / history-space crossover: by flops h = d, but at Dp <= 256 the
   // d-space kernel overtakes the TH = 8 bucket (225 < h <= 256) in time (epoch
   // 15.6 -> 15.1 ms at the ML-20M shape, threshold sweep in DESIGN.md 3.2); at
@@ -564,6 +642,7 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
 void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  if (c->stream5) (void)hipStreamSynchronize(c->stream5);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
   for (int s = 0; s < 3; ++s) {
@@ -621,6 +700,9 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
     (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamDestroy(c->stream2);
   }
+  for (hipEvent_t e : {c->ev_pre5, c->ev_eager[0], c->ev_eager[1]})
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream5) (void)hipStreamDestroy(c->stream5);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -644,6 +726,10 @@ int frecsys_comm_init(frecsys_ctx* c, int32_t world, int32_t rank, const uint8_t
     ncclCommDestroy(c->comm);
     c->comm = nullptr;
   }
+  int rc = join_eager(c, 3, c->stream);
+  if (rc) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->gram_src[0] = c->gram_src[1] = 0;  // partials now sum over other shards
   c->world = world;
   c->rank = rank;
   if (id) {  // a communicator at every world size (world 1: the exchange path still runs)
@@ -684,6 +770,13 @@ int frecsys_load_csr(frecsys_ctx* c, int32_t side, int64_t n_rows, const int64_t
       return fail(c, FRECSYS_ERR_INVALID,
                   "frecsys_load_csr: column id " + std::to_string(col[k]) + " out of range");
   HIP_TRY(c, hipSetDevice(c->device));
+  {
+    int rc = join_eager(c, 3, c->stream);
+    if (rc) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  c->gram_src[0] = c->gram_src[1] = 0;
+  if (side == 2) emb_written(c, 2);
   if (c->rp[side]) HIP_TRY(c, hipFree(c->rp[side]));
   if (c->col[side]) HIP_TRY(c, hipFree(c->col[side]));
   c->rp[side] = nullptr;
@@ -719,6 +812,9 @@ int frecsys_set_embeddings(frecsys_ctx* c, int32_t side, const float* host, int6
     return fail(c, FRECSYS_ERR_INVALID, "frecsys_set_embeddings: bad arguments");
   if (!c->emb[side]) return fail(c, FRECSYS_ERR_INVALID, "side has no embeddings yet");
   HIP_TRY(c, hipSetDevice(c->device));
+  int rc = join_eager(c, 3, c->stream);
+  if (rc) return rc;
+  emb_written(c, side);
   const int64_t rows = c->n[side];
   HIP_TRY(c, hipMemsetAsync(c->emb[side], 0, sizeof(float) * std::max<int64_t>(rows, 1) * c->Dp,
                             c->stream));
@@ -777,10 +873,25 @@ int frecsys_gramian(frecsys_ctx* c, int32_t side, const float* weights, int32_t 
   if (from_snapshot && !c->snap[side])
     return fail(c, FRECSYS_ERR_INVALID, "gramian: no snapshot taken");
   HIP_TRY(c, hipSetDevice(c->device));
+  int rc;
+  const bool plain = !weights && !from_snapshot;
+  if (plain && c->gram_src[side] != 0 && c->gram_src[side] == c->emb_ver[side]) {
+    // the embeddings are unchanged since this Gramian was formed: the same
+    // deterministic computation would write the same bits (on every rank)
+    if (host_out)
+      HIP_TRY(c, hipMemcpy2DAsync(host_out, sizeof(float) * c->dim, c->gram[side],
+                                  sizeof(float) * c->Dp, sizeof(float) * c->dim, c->dim,
+                                  hipMemcpyDeviceToHost, c->stream));
+    rc = maybe_start_eager(c, side);
+    if (rc) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return FRECSYS_OK;
+  }
+  rc = join_eager(c, 1 << side, c->stream);  // an early basis build still reading this G
+  if (rc) return rc;
   int64_t lo, hi;
   shard(c, side, &lo, &hi);
   const int64_t rows = hi - lo;
-  int rc;
   const float* dw = nullptr;
   if (weights) {
     rc = upload(c, &c->d_gram_w, &c->cap_gram_w, weights, (size_t)c->n[side]);
@@ -807,10 +918,14 @@ int frecsys_gramian(frecsys_ctx* c, int32_t side, const float* weights, int32_t 
                               ncclSum, c->comm, c->stream));
     t.stop();
   }
+  c->gram_ver[side] = ++c->ver_counter;
+  c->gram_src[side] = plain ? c->emb_ver[side] : 0;
   if (host_out)
     HIP_TRY(c, hipMemcpy2DAsync(host_out, sizeof(float) * c->dim, c->gram[side],
                                 sizeof(float) * c->Dp, sizeof(float) * c->dim, c->dim,
                                 hipMemcpyDeviceToHost, c->stream));
+  rc = maybe_start_eager(c, side);
+  if (rc) return rc;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FRECSYS_OK;
 }
@@ -819,6 +934,10 @@ int frecsys_set_gramian(frecsys_ctx* c, int32_t side, const float* host, int64_t
   if (!c || side < 0 || side > 1 || !host || ld < c->dim)
     return fail(c, FRECSYS_ERR_INVALID, "set_gramian: bad arguments");
   HIP_TRY(c, hipSetDevice(c->device));
+  int rc = join_eager(c, 1 << side, c->stream);
+  if (rc) return rc;
+  c->gram_ver[side] = ++c->ver_counter;
+  c->gram_src[side] = 0;
   HIP_TRY(c, hipMemsetAsync(c->gram[side], 0, sizeof(float) * c->Dp * c->Dp, c->stream));
   HIP_TRY(c, hipMemcpy2DAsync(c->gram[side], sizeof(float) * c->Dp, host, sizeof(float) * ld,
                               sizeof(float) * c->dim, c->dim, hipMemcpyHostToDevice, c->stream));
@@ -896,7 +1015,8 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
   if (p->from_snapshot && !c->snap[other])
     return fail(c, FRECSYS_ERR_INVALID, "solve: from_snapshot without a snapshot");
   HIP_TRY(c, hipSetDevice(c->device));
-  int rc;
+  int rc = join_eager(c, side < 2 ? 1 << side : 0, c->stream);  // a build still reading emb[side]
+  if (rc) return rc;
   if (ukind && p->entity_weight) {
     rc = upload(c, &c->d_entity_weight, &c->cap_entity_weight, p->entity_weight,
                 (size_t)c->n[side]);
@@ -971,6 +1091,8 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
   const bool dual = c->dual_on && !force_dspace && m_spd && !grad && c->Dp >= 64 &&
                     c->dual_max_h > 0 && (int64_t)hs.size() == c->order_n[side];
   const int64_t n_dspace = dual ? first_le(c->dual_max_h) : a.n_rows;
+  c->dual_used[side] = dual;
+  if (side < 2) emb_written(c, side);
   const int64_t n_nonempty = dual ? first_le(0) : a.n_rows;
   {
     static const char* names[3] = {"solve_user", "solve_item", "solve_eval"};
@@ -1274,6 +1396,11 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
     return fail(c, FRECSYS_ERR_INVALID, "pp_step: WEIGHTED_V needs entity_reg and other_weight");
   HIP_TRY(c, hipSetDevice(c->device));
   const int other = side == 1 ? 0 : 1;
+  {
+    int rc = join_eager(c, 3, c->stream);
+    if (rc) return rc;
+  }
+  if (side < 2) emb_written(c, side);
   if (kind == FRECSYS_KIND_WEIGHTED_U && p->entity_weight) {
     int rc = upload(c, &c->d_entity_weight, &c->cap_entity_weight, p->entity_weight,
                     (size_t)c->n[side]);
@@ -1411,6 +1538,7 @@ int frecsys_train_stats(frecsys_ctx* c, double* observed, double* unobserved,
 int frecsys_synchronize(frecsys_ctx* c) {
   if (!c) return FRECSYS_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream5));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FRECSYS_OK;
 }

@@ -42,8 +42,10 @@ def test_world1_rccl_matches_no_comm(quirk_data, dim):
     ctx, _, _ = _ctx(dim, nu, ni, up, uc, ip, ic)
     ctx.comm_init(1, 0, fh.unique_id())
     got = _epoch(ctx, nu, ni, up, ip, ic)
-    # every collective site ran through RCCL
-    assert ctx.timing("allreduce")[1] >= 5
+    # every collective site ran through RCCL (the closing plain Gramian of the
+    # item side repeats the one before the loss on unchanged rows: reused,
+    # no all-reduce -- every rank makes the same reuse decision)
+    assert ctx.timing("allreduce")[1] >= 4
     assert ctx.timing("allgather")[1] >= 4
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)
