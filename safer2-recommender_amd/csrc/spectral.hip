@@ -431,24 +431,36 @@ __global__ void __launch_bounds__(256)
   };
   float vn[8];
   load_a(0, vn);
-#pragma unroll 4
+  // B fragments (the Q pieces, L2-resident) one k-step ahead as well
+  bf16x8 bn[CW][3];
+  auto load_b = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const int C = C0 + j < NCT ? C0 + j : NCT - 1;  // clamped: no branch around the loads
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bn[j][p] = Bs[((int64_t)(s * NCT + C) * 3 + p) * 64 + lane];
+    }
+  };
+  load_b(0);
+#pragma unroll 2
   for (int s = 0; s < NS; ++s) {
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = vn[j];
-    if (s + 1 < NS) load_a(s + 1, vn);  // next step's rows in flight
+    bf16x8 bf[CW][3];
+#pragma unroll
+    for (int j = 0; j < CW; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bf[j][p] = bn[j][p];
+    if (s + 1 < NS) {  // next step's rows and Q pieces in flight
+      load_a(s + 1, vn);
+      load_b(s + 1);
+    }
     bf16x8 af[3];
     split3x8(v, af);
 #pragma unroll
-    for (int j = 0; j < CW; ++j) {
-      const int C = C0 + j;
-      if (C < NCT) {  // wave-uniform
-        bf16x8 bf[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p) bf[p] = Bs[((int64_t)(s * NCT + C) * 3 + p) * 64 + lane];
-        acc[j] = mfma_x6(af, bf, acc[j]);
-      }
-    }
+    for (int j = 0; j < CW; ++j)
+      if (C0 + j < NCT) acc[j] = mfma_x6(af, bf[j], acc[j]);  // wave-uniform
   }
   if (qpart) {
     // u^T B u partials of the user loss (B = G): row dots of (X B) with X
