@@ -127,42 +127,44 @@ __global__ void __launch_bounds__(GramCfg<T>::NTHR)
 }
 
 // Sum of the nblk partial slabs, four consecutive elements (one float4) of
-// the lower tiles per thread.  The blocks are cut into kRedChains contiguous
-// ranges summed as independent chains (many loads in flight per thread: the
-// read is bandwidth-, not latency-bound), then combined in chain order -- a
-// fixed order, so the result is deterministic.  Then mirrored into G.
+// the lower tiles per output.  The blocks are cut into kRedChains contiguous
+// ranges summed as independent chains -- one thread per (chain, float4), so
+// 8 x NT workgroups share the read (bandwidth-, not latency-bound: 36 one-
+// chain-set workgroups left 220 CUs idle, 102 us) -- then combined in chain
+// order through LDS: a fixed order, so the result is deterministic.  Then
+// mirrored into G.
 constexpr int kRedChains = 8;
 template <int T>
 __global__ void __launch_bounds__(256)
     gram_reduce_kernel(const float* __restrict__ P, int64_t nblk, float* __restrict__ G) {
-  constexpr int Dp = 32 * T, NT = T * (T + 1) / 2;
-  const int q = blockIdx.x * 256 + threadIdx.x;  // float4 index within a slab
-  if (q >= NT * 256) return;
+  constexpr int Dp = 32 * T, NT = T * (T + 1) / 2, QW = 256 / kRedChains;
+  __shared__ float4 part[kRedChains][QW];
+  const int c = threadIdx.x / QW, qq = threadIdx.x % QW;
+  const int q = blockIdx.x * QW + qq;  // float4 index within a slab (NT * 256 is a multiple of QW)
   const int64_t stride = (int64_t)NT * 1024;
-  float4 acc[kRedChains];
   const int64_t per = (nblk + kRedChains - 1) / kRedChains;
-#pragma unroll
-  for (int c = 0; c < kRedChains; ++c) acc[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t i = 0; i < per; ++i) {
-#pragma unroll
-    for (int c = 0; c < kRedChains; ++c) {
-      const int64_t b = c * per + i;
-      if (b < nblk) {
-        const float4 v = reinterpret_cast<const float4*>(P + b * stride)[q];
-        acc[c].x += v.x;
-        acc[c].y += v.y;
-        acc[c].z += v.z;
-        acc[c].w += v.w;
-      }
+    const int64_t b = c * per + i;
+    if (b < nblk) {
+      const float4 v = reinterpret_cast<const float4*>(P + b * stride)[q];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
     }
   }
-  float4 s = acc[0];
+  part[c][qq] = acc;
+  __syncthreads();
+  if (c != 0) return;
+  float4 s = part[0][qq];
 #pragma unroll
-  for (int c = 1; c < kRedChains; ++c) {
-    s.x += acc[c].x;
-    s.y += acc[c].y;
-    s.z += acc[c].z;
-    s.w += acc[c].w;
+  for (int k = 1; k < kRedChains; ++k) {
+    const float4 v = part[k][qq];
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
   }
   const int t = q >> 8, e0 = (q & 255) * 4;  // tile, first element (row-major 32 x 32)
   int I = 0;
@@ -220,7 +222,7 @@ hipError_t launch_tiled(const GramArgs& a, hipStream_t s) {
   else
     return hipMemsetAsync(a.G, 0, sizeof(float) * Dp * Dp, s);
   constexpr int NT = T * (T + 1) / 2;
-  hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3((NT * 256 + 255) / 256), dim3(256), 0, s,
+  hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3(NT * 256 / (256 / kRedChains)), dim3(256), 0, s,
                      a.partials, nblk, a.G);
   return hipGetLastError();
 }
