@@ -994,6 +994,9 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
             "epilogue %.0f (rhs %.0f tiles %.0f) chol %.0f | chain %.0f workers %.0f factored %.0f\n",
             pre.c_str(), hp[4], hp[8] / n, hp[0] / n, hp[1] / n, (hp[2] + hp[9] + hp[10]) / n,
             hp[9] / n, hp[10] / n, hp[3] / n, hp[5] / n, hp[6] / n, hp[7] / n);
+    fprintf(stderr, "[dspace-prof] %s chain: waits %.0f trsm %.0f update %.0f factor %.0f | "
+            "worker waits %.0f\n",
+            pre.c_str(), hp[11] / n, hp[12] / n, hp[13] / n, hp[14] / n, hp[15] / n);
   }
   return FRECSYS_OK;
 }

@@ -72,7 +72,9 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
   const bool fl = lane < 32;
   float a[32];
   load_factor_rows<1>(tile, r, fl, a);
-  bool ok = true;
+  // pivot test on the scalar unit: piv > 0 and not NaN <=> its bits as an
+  // int lie in (0, 0x7f800000]
+  int pmin = 0x7fffffff, pmax = 0;
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
     float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
@@ -90,7 +92,9 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
     }
     const float t = a[k] - ((p0 + p1) + (p2 + p3));
     const float piv = rdlane(t, k);
-    ok = ok && (piv > 0.0f);
+    const int pi = __builtin_amdgcn_readfirstlane(__float_as_int(piv));
+    pmin = min(pmin, pi);
+    pmax = max(pmax, pi);
     // v_rsq_f32 (1 ulp) instead of the IEEE sqrt + divide sequences on the
     // serial chain
     const float rd = __builtin_amdgcn_rsqf(piv);
@@ -101,7 +105,7 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
 #pragma unroll
   for (int k = 0; k < 32; ++k)
     if (!fl) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
-  return ok;
+  return pmin > 0 && pmax <= 0x7f800000;
 }
 
 // Blocked form of the same factor + inverse: columns 0..15 by the
@@ -119,23 +123,25 @@ __device__ __noinline__ bool diag_factor_inv_blk(lds_float* tile, int lane) {
   const bool fl = lane < 32;
   float a[32];
   load_factor_rows<8>(tile, r, fl, a);
-  bool ok = true;
+  // pivot test without a vector compare per column: piv > 0 and not NaN
+  // <=> its bits as an int lie in (0, 0x7f800000]
+  int pmin = 0x7fffffff, pmax = 0;
   auto column = [&](int k, int m0) {  // column k from the terms m in [m0, k)
-    float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+    // two partial sums (one v_pk_fma_f32 per pair of terms, one add to
+    // combine): this one wave's instruction count is the chain's bound
+    float p0 = 0.f, p1 = 0.f;
 #pragma unroll
-    for (int m = m0; m < k; m += 4) {
+    for (int m = m0; m < k; m += 2) {
       const float b0 = rdlane(a[m], k);
       const float b1 = m + 1 < k ? rdlane(a[m + 1], k) : 0.0f;
-      const float b2 = m + 2 < k ? rdlane(a[m + 2], k) : 0.0f;
-      const float b3 = m + 3 < k ? rdlane(a[m + 3], k) : 0.0f;
       p0 += a[m] * b0;
       if (m + 1 < k) p1 += a[m + 1] * b1;
-      if (m + 2 < k) p2 += a[m + 2] * b2;
-      if (m + 3 < k) p3 += a[m + 3] * b3;
     }
-    const float t = a[k] - ((p0 + p1) + (p2 + p3));
+    const float t = a[k] - (p0 + p1);
     const float piv = rdlane(t, k);
-    ok = ok && (piv > 0.0f);
+    const int pi = __builtin_amdgcn_readfirstlane(__float_as_int(piv));
+    pmin = min(pmin, pi);
+    pmax = max(pmax, pi);
     a[k] = t * __builtin_amdgcn_rsqf(piv);  // lane k: t = piv -> sqrt(piv)
   };
 #pragma unroll
@@ -179,9 +185,18 @@ __device__ __noinline__ bool diag_factor_inv_blk(lds_float* tile, int lane) {
   for (int k = 16; k < 32; ++k) column(k, 16);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   const int j = r;
+  const bool ok = pmin > 0 && pmax <= 0x7f800000;
+  if (ok) {
+    // entries k < j of column j of L^-1 came out of the recurrence as +-0
+    // (zero inputs times finite factors): stored as they are
 #pragma unroll
-  for (int k = 0; k < 32; ++k)
-    if (!fl) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
+    for (int k = 0; k < 32; ++k)
+      if (!fl) tile[sw(k, j)] = a[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (!fl) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
+  }
   return ok;
 }
 
@@ -442,17 +457,37 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   if (wave == 0) {
     // ---- the critical chain (issue priority over the worker on its SIMD) ----
     __builtin_amdgcn_s_setprio(2);
+    // diagnostics (prof): chain cycles in waits / TRSM / update / factor
+    unsigned long long tw = 0, ts = 0, tu = 0, tf = 0, tc = prof ? clock64() : 0;
+    auto lap = [&](unsigned long long& acc) {
+      if (prof) {
+        const unsigned long long t = clock64();
+        acc += t - tc;
+        tc = t;
+      }
+    };
 #pragma unroll 1
     for (int p = -1; p + 1 < T; ++p) {  // one factor call site
       if (p >= 0) {
         wait_ver(ver + tidx(p + 1, p), p);  // all of panel < p's updates
+        lap(tw);
         trsm(p + 1, p);
         if (!YW) bupd(p + 1, p);
+        lap(ts);
         wait_ver(ver + tidx(p + 1, p + 1), p);
+        lap(tw);
         update(p + 1, p + 1, p);
+        lap(tu);
       }
       factor(p + 1);
       if (!YW) ysolve(p + 1);
+      lap(tf);
+    }
+    if (prof && lane == 0) {
+      atomicAdd(prof + 11, tw);
+      atomicAdd(prof + 12, ts);
+      atomicAdd(prof + 13, tu);
+      atomicAdd(prof + 14, tf);
     }
     __builtin_amdgcn_s_setprio(0);
     if (prof && lane == 0) atomicAdd(prof + 5, clock64() - t0);
@@ -471,15 +506,25 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   } else {
     // ---- workers: the rest of each panel, round-robin ----
     int k = 0;
+    unsigned long long tww = 0;  // diagnostics (prof): cycles in waits
+    auto wwait = [&](const int* f, int v) {
+      if (prof) {
+        const unsigned long long t = clock64();
+        wait_ver(f, v);
+        tww += clock64() - t;
+      } else {
+        wait_ver(f, v);
+      }
+    };
 #pragma unroll 1
     for (int p = 0; p + 1 < T; ++p) {
 #pragma unroll 1
       for (int I = p + 2; I < T; ++I, ++k) {  // S(I, p), B(I, p)
         if (W0 + k % (NW - W0) != wave) continue;
-        wait_ver(ver + tidx(p, p), p + 1);
-        wait_ver(ver + tidx(I, p), p);
+        wwait(ver + tidx(p, p), p + 1);
+        wwait(ver + tidx(I, p), p);
         trsm(I, p);
-        wait_ver(yver, p + 1);
+        wwait(yver, p + 1);
         bupd(I, p);
       }
 #pragma unroll 1
@@ -487,14 +532,17 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
 #pragma unroll 1
         for (int I = (J == p + 1 ? p + 2 : J); I < T; ++I, ++k) {
           if (W0 + k % (NW - W0) != wave) continue;
-          wait_ver(ver + tidx(I, p), p + 1);
-          wait_ver(ver + tidx(J, p), p + 1);
-          wait_ver(ver + tidx(I, J), p);
+          wwait(ver + tidx(I, p), p + 1);
+          wwait(ver + tidx(J, p), p + 1);
+          wwait(ver + tidx(I, J), p);
           update(I, J, p);
         }
       }
     }
-    if (prof && lane == 0) atomicAdd(prof + 6, (clock64() - t0) / (NW - W0));
+    if (prof && lane == 0) {
+      atomicAdd(prof + 6, (clock64() - t0) / (NW - W0));
+      atomicAdd(prof + 15, tww / (NW - W0));
+    }
   }
   lds_barrier();
   if (prof && tid == 0) atomicAdd(prof + 7, clock64() - t0);
