@@ -277,22 +277,24 @@ int build_order(frecsys_ctx* c, int side) {
 }
 
 // Long-history split of the d-space queue prefix [0, n): entities with
-// more than 2*split_rows assembly rows get their SYRK cut into split_rows
-// slabs done by separate workgroups (launch_split_syrk) before the solve.
+// more than 2*C assembly rows get their SYRK cut into C-row slabs done by
+// separate workgroups (launch_split_syrk / wide_syrk2_kernel<2>) before the
+// solve; at most max_slabs slabs of slab_floats each (longest entities first).
 int plan_split(frecsys_ctx* c, const std::vector<int32_t>& hs, int64_t n,
-               const std::function<int64_t(int64_t)>& heff, SolveArgs* a) {
+               const std::function<int64_t(int64_t)>& heff, SolveArgs* a, int64_t C,
+               size_t slab_floats, int64_t max_slabs) {
   a->split = nullptr;
   a->n_split = 0;
   a->slabs = nullptr;
   a->work = nullptr;
   a->n_work = 0;
-  const int64_t C = c->split_rows;
-  if (C <= 0 || c->Dp < 32) return FRECSYS_OK;
+  if (c->split_rows <= 0 || C <= 0 || c->Dp < 32) return FRECSYS_OK;
   c->h_split.clear();
   c->h_work.clear();
   int32_t slab = 0;
   for (int64_t i = 0; i < n && heff(hs[i]) > 2 * C; ++i) {
     const int64_t ne = heff(hs[i]);
+    if (slab + (ne + C - 1) / C > max_slabs) break;
     const int32_t first = slab;
     for (int64_t k = 0; k < ne; k += C)
       c->h_work.push_back(SplitWork{(int32_t)i, (int32_t)k, (int32_t)std::min(ne, k + C), slab++});
@@ -303,7 +305,7 @@ int plan_split(frecsys_ctx* c, const std::vector<int32_t>& hs, int64_t n,
   if (rc) return rc;
   rc = ensure(c, &c->d_work, &c->cap_work, c->h_work.size());
   if (rc) return rc;
-  rc = ensure(c, &c->d_slabs, &c->cap_slabs, (size_t)slab * split_slab_floats(c->Dp));
+  rc = ensure(c, &c->d_slabs, &c->cap_slabs, (size_t)slab * slab_floats);
   if (rc) return rc;
   HIP_TRY(c, hipMemcpy(c->d_split, c->h_split.data(), sizeof(int2) * c->h_split.size(),
                        hipMemcpyHostToDevice));
@@ -960,13 +962,20 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
     const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(ap.n_rows, budget));
     int rc = ensure(c, &c->wide_ws, &c->cap_wide_ws, (size_t)batch * slot);
     if (rc) return rc;
+    if (can_split) {  // long histories of the first batch cut into slabs (same budget)
+      const size_t sf = wide_slab_floats(c->Dp);
+      rc = plan_split(c, hs, batch, heff, &ap, wide_slab_rows(), sf,
+                      (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (sf * sizeof(float))));
+      if (rc) return rc;
+    }
     const size_t k = ktimer_begin(c, pre + ".dspace", s);
     HIP_TRY(c, launch_wide_solve(c->Dp, ap, c->wide_ws, batch, s));
     ktimer_end(c, k, s);
     return FRECSYS_OK;
   }
   if (can_split) {
-    int rc = plan_split(c, hs, ap.n_rows, heff, &ap);
+    int rc = plan_split(c, hs, ap.n_rows, heff, &ap, c->split_rows, split_slab_floats(c->Dp),
+                        INT64_MAX);
     if (rc) return rc;
   }
   if (ap.n_work > 0) {

@@ -47,7 +47,7 @@ struct SolveArgs {
   unsigned long long* fail;    // atomicMin(entity + 1) on a non-SPD pivot
   int debug_skip;              // diagnostic ablation mask (0 in production)
   unsigned long long* prof;    // diagnostics: per-phase cycle sums [16] (nullptr = off)
-  // long-history split (tiled kernel only; nullptr / 0 = none)
+  // long-history split (tiled and wide kernels; nullptr / 0 = none)
   const int2* split;           // [n_split] per queue position: first slab, slab count
   int64_t n_split;
   float* slabs;                // [slabs][split_slab_floats(Dp)]
@@ -207,6 +207,13 @@ hipError_t launch_eval_topk(const float* X, int64_t r0, int64_t n, const float* 
 // wide_quad_floats partials).
 bool wide_dim(int Dp);
 size_t wide_slot_floats(int Dp);
+// Long-history split of the wide d-space SYRK: entities of the first batch
+// with more than 2 * wide_slab_rows() assembly rows have their SYRK cut into
+// slabs of wide_slab_rows() (the two-level accumulation block, so the slab
+// sums fold into exactly the unsplit result) in a.work / a.split / a.slabs
+// ([slabs][wide_slab_floats(Dp)]), computed by their own workgroups first.
+int64_t wide_slab_rows();
+size_t wide_slab_floats(int Dp);
 int64_t wide_gram_num_blocks(int64_t n);
 hipError_t launch_wide_gramian(int Dp, const GramArgs& g, hipStream_t s);
 hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batch,

@@ -147,16 +147,22 @@ __global__ void __launch_bounds__(512)
   // a diagonal pair stages one block (A = B) unless its B side is weighted
   const bool same = dgp && !(MODE == 0 && g.w != nullptr);
   const int kind = a.kind;
-  const bool vk = MODE == 1 && is_v_kind(kind);
+  const bool vk = MODE >= 1 && is_v_kind(kind);
 
-  int64_t r0 = 0, nrow = 0, e = 0, h = 0, p0 = 0;
+  // MODE 2 unit = one slab (rows [k0, k1) of a long history) of a.work;
+  // MODE 1 units below a.n_split fold their slabs instead of gathering
+  int64_t r0 = 0, nrow = 0, e = 0, h = 0, p0 = 0, kbase = 0, klim = 0;
+  bool fin = false;
   if (MODE == 0) {
     r0 = g.row0 + unit * rpb;
     int64_t r1 = r0 + rpb;
     if (r1 > g.row0 + g.n) r1 = g.row0 + g.n;
     nrow = r1 > r0 ? r1 - r0 : 0;
+    klim = nrow;
   } else {
-    const QueueRec rec = a.order[pos0 + unit];
+    SplitWork sw{};
+    if (MODE == 2) sw = a.work[unit];
+    const QueueRec rec = a.order[MODE == 2 ? (int64_t)sw.pos : pos0 + unit];
     e = rec.entity;
     h = rec.h;
     p0 = rec.p0;
@@ -164,15 +170,22 @@ __global__ void __launch_bounds__(512)
     int64_t extra = 0;
     if (vk && a.quirk && h > 128 && (h % 128) != 0) extra = 128 - (h % 128);
     nrow = h + extra;
+    klim = nrow;
+    if (MODE == 2) {
+      kbase = sw.k0;
+      klim = sw.k1;
+    } else {
+      fin = pos0 + unit < a.n_split;
+    }
   }
-  const int nchunks = (int)((nrow + W2R - 1) / W2R);
+  const int nchunks = fin ? 0 : (int)((klim - kbase + W2R - 1) / W2R);
 
   auto ring_load = [&](int c, int& id, float& sa, float& bw) __attribute__((always_inline)) {
-    const int64_t k = (int64_t)c * W2R + tid;
+    const int64_t k = kbase + (int64_t)c * W2R + tid;
     id = -1;
     sa = 0.0f;
     bw = 0.0f;
-    if (k < nrow) {
+    if (k < klim) {
       if (MODE == 0) {
         id = (int)(r0 + k);
         sa = 1.0f;
@@ -201,7 +214,7 @@ __global__ void __launch_bounds__(512)
   const int hh0 = same ? (tid >> 8) : 0;
   const int xcol = sc < WB2 ? WB2 * BI + sc : WB2 * BJ + (sc - WB2);
   const bool wside = MODE == 0 && !same && sc >= WB2;  // weighted B operand
-  const bool bown = MODE == 1 && dgp;                  // diagonal pairs form b
+  const bool bown = MODE >= 1 && dgp;                  // diagonal pairs form b
   float xr[16];
   auto load = [&](int c) __attribute__((always_inline)) {
     const int base = (c % W2RING) * W2R + 8 * hh0;
@@ -225,6 +238,9 @@ __global__ void __launch_bounds__(512)
   // staging math of one value (row r of the thread's column): scale, rhs
   // part, 3-piece split into the fragment being assembled
   auto stage_val = [&](int base, int r, bf16x8 (&f)[3], int j) __attribute__((always_inline)) {
+    // no contraction: x is the rounded fp32 product in every instantiation
+    // (fused into split3's x - hi it would depend on the code around it)
+#pragma clang fp contract(off)
     const float2 sb = ring_sb[base + r];
     float x = xr[r] * sb.x;
     if (bown) bpart += sb.y * x;
@@ -260,8 +276,9 @@ __global__ void __launch_bounds__(512)
   };
   const int boff = same ? 0 : WB2;  // B operand columns in the staged image
 
-  float* const otile0 = MODE == 0 ? g.partials + unit * NT * 1024
-                                  : ws + unit * ((int64_t)NT * 1024 + Dp);
+  float* const otile0 = MODE == 0   ? g.partials + unit * NT * 1024
+                        : MODE == 1 ? ws + unit * ((int64_t)NT * 1024 + Dp)
+                                    : nullptr;  // MODE 2 never flushes (<= W2FLUSH chunks)
   auto otile = [&](int m) __attribute__((always_inline)) {
     return otile0 + (int64_t)tidx(8 * BI + tI, 8 * BJ + m) * 1024;
   };
@@ -283,8 +300,6 @@ __global__ void __launch_bounds__(512)
       acc[m] = f32x16{0.f};
       __builtin_amdgcn_sched_barrier(0);
     }
-    btot += bpart;
-    bpart = 0.0f;
     flushed = true;
   };
 
@@ -323,6 +338,12 @@ __global__ void __launch_bounds__(512)
       const bf16x8* st = stage[buf];
       bf16x8* sto = stage[buf ^ 1];
       const int nbase = ((c + 1) % W2RING) * W2R + 8 * hh0;
+      // b's block boundary matches the tiles' (chunks <= c; chunk c+1 is
+      // staged below), so 2048-row slabs fold into the same sums
+      if ((c + 1) % W2FLUSH == 0 && more) {  // block-uniform
+        btot += bpart;
+        bpart = 0.0f;
+      }
       // A fragments of the wave's tile row, shared by its tiles; B fragments
       // one tile ahead of their MFMAs
       bf16x8 af[3], bcur[3], bnxt[3], fs[3];
@@ -373,6 +394,51 @@ __global__ void __launch_bounds__(512)
         for (int q = 0; q < 16; ++q) acc[m][q] += t[acc_row(q, hi) * 32 + lo];
       }
       __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // slab layout: tile t's accumulator q of lane l at t * 1024 + q * 64 + l
+  // (coalesced); b partials of the diagonal pairs' threads after the tiles
+  const size_t slab_floats = (size_t)NT * 1024 + 2 * (size_t)Dp;
+  auto stile = [&](const float* sb, int m) __attribute__((always_inline)) {
+    return sb + (int64_t)tidx(8 * BI + tI, 8 * BJ + m) * 1024 + lane;
+  };
+  if (MODE == 2) {
+    float* sb = a.slabs + (size_t)a.work[unit].slab * slab_floats;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (tv(m)) {
+        float* t = const_cast<float*>(stile(sb, m));
+#pragma unroll
+        for (int q = 0; q < 16; ++q) t[q * 64] = acc[m][q];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (bown) sb[(size_t)NT * 1024 + WB2 * 2 * BI + tid] = bpart;
+    return;
+  }
+  if (MODE == 1 && fin) {
+    // the unsplit kernel's two-level sum: block sums folded left to right
+    // (t = s_1, t = t + s_j, ..., s_last + t), b likewise from 0
+    const int2 sp = a.split[pos0 + unit];
+#pragma unroll 1
+    for (int j = 0; j < sp.y; ++j) {
+      const float* sb = a.slabs + (size_t)(sp.x + j) * slab_floats;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        if (tv(m)) {
+          const float* t = stile(sb, m);
+          f32x16 v;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] = t[q * 64];
+          acc[m] = j == 0 ? v : acc[m] + v;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (bown) {
+        const float bv = sb[(size_t)NT * 1024 + WB2 * 2 * BI + tid];
+        if (j + 1 < sp.y) btot += bv;
+        else bpart = bv;
+      }
     }
   }
   bpart += btot;
@@ -626,26 +692,37 @@ __global__ void __launch_bounds__(512)
   // ---- back substitution x_p = L_pp^-T (y_p - sum_{q>p} L_qp^T x_q) ----
 #pragma unroll 1
   for (int p = T - 1; p >= 0; --p) {
+    // every workspace load of the step is issued before the first use (the
+    // x-independent L values: one HBM round trip per step instead of one per
+    // four values); the summation orders are unchanged
+    float li[32];
+    if (wave == 0) {
+      const float* Li = gtile(p, p);
+#pragma unroll
+      for (int i = 0; i < 32; ++i) li[i] = Li[i * 32 + lo];
+    }
     float pr = 0.0f;
     for (int q = p + 1 + wave; q < T; q += NW) {
-      const float* L = gtile(q, p);
-#pragma unroll 4
-      for (int mm = 16 * hi; mm < 16 * hi + 16; ++mm) pr += L[mm * 32 + lo] * xv[32 * q + mm];
+      const float* L = gtile(q, p) + 16 * hi * 32 + lo;
+      float lv[16];
+#pragma unroll
+      for (int mm = 0; mm < 16; ++mm) lv[mm] = L[mm * 32];
+#pragma unroll
+      for (int mm = 0; mm < 16; ++mm) pr += lv[mm] * xv[32 * q + 16 * hi + mm];
     }
     pr += __shfl_xor(pr, 32);
     if (hi == 0) part[wave * 32 + lo] = pr;
-    __syncthreads();
+    lds_barrier();
     if (wave == 0) {
       float r = yv[32 * p + lo];
 #pragma unroll
       for (int w = 0; w < NW; ++w) r -= part[w * 32 + lo];
-      const float* Li = gtile(p, p);
       float x = 0.0f;
-#pragma unroll 8
-      for (int i = 0; i < 32; ++i) x += Li[i * 32 + lo] * rdlane(r, i);
+#pragma unroll
+      for (int i = 0; i < 32; ++i) x += li[i] * rdlane(r, i);
       if (hi == 0) xv[32 * p + lo] = x;
     }
-    __syncthreads();
+    lds_barrier();
   }
   for (int i = tid; i < Dp; i += 512) a.out[e * Dp + i] = xv[i];
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
@@ -888,6 +965,13 @@ size_t wide_slot_floats(int Dp) {
   return (size_t)T * (T + 1) / 2 * 1024 + Dp;
 }
 
+int64_t wide_slab_rows() { return (int64_t)W2FLUSH * W2R; }
+
+size_t wide_slab_floats(int Dp) {
+  const int T = Dp >> 5;
+  return (size_t)T * (T + 1) / 2 * 1024 + 2 * (size_t)Dp;
+}
+
 int64_t wide_gram_num_blocks(int64_t n) {
   const int64_t rpb = wide_rows_per_block(n);
   return (n + rpb - 1) / rpb;
@@ -928,6 +1012,12 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
   }
   const bool grad = is_grad_kind(a.kind);
   GramArgs g{};
+  // the slabs of the long histories (all in the first batch) first
+  if (a.n_work > 0) {
+    if (a.n_split > std::min<int64_t>(batch, a.n_rows)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wide_syrk2_kernel<2>, dim3(xcd_grid(a.n_work, wide_pairs2(Dp))), dim3(512),
+                       0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
+  }
   for (int64_t s0 = 0; s0 < a.n_rows; s0 += batch) {
     const int64_t nb = std::min<int64_t>(batch, a.n_rows - s0);
     hipLaunchKernelGGL(wide_syrk2_kernel<1>, dim3(xcd_grid(nb, wide_pairs2(Dp))), dim3(512), 0, s,
