@@ -326,8 +326,9 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
         "u_halfstep_solve_updates_per_s": ((uhi - ulo) / (su_ms * 1e-3)) * world if su_ms else None,
         "kernel_ms_per_epoch": {k: v[0] / max(K, 1) for k, v in timers.items()},
         "roofline": {"bound": "mfma",
-                     "kernel": ("wide_syrk_kernel + wide_chol_kernel (batched d-space solve, "
-                                "A in an HBM workspace)") if wide else
+                     "kernel": ("wide_syrk2_kernel<2> (slabs of the long histories) + "
+                                "wide_syrk2_kernel<1> + wide_chol_kernel<16> (batched d-space "
+                                "solve, A in an HBM workspace)") if wide else
                                ("solve_tiled_kernel<8, false, true> (d-space solve: split-bf16 "
                                 "MFMA SYRK + fp32 dataflow Cholesky)"),
                      "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
