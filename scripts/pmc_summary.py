@@ -30,7 +30,9 @@ def per_kernel(path, counter):
 
 def dominant(name, workload):
     if "d512" in workload or "d1024" in workload:
-        return "wide_syrk_kernel<1" in name or "wide_chol_kernel" in name
+        # the batched d-space call: slab SYRK, entity SYRK and Cholesky launches
+        return any(k in name for k in ("wide_syrk2_kernel<1>", "wide_syrk2_kernel<2>",
+                                       "wide_chol_kernel"))
     return "solve_tiled_kernel<8, false" in name
 
 
