@@ -1,0 +1,30 @@
+"""Diagnostic: one wide (d=512) iALS item and weighted-U user solve on the
+tests/test_wide_split_gpu.py fixture, saved to <out>.npz (for bit-for-bit
+comparisons between library builds)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+for p in ("tests", "oracle", "safer2-recommender_amd"):
+    sys.path.insert(0, os.path.join(ROOT, p))
+import frecsys_hip as fh  # noqa: E402
+from test_parity_gpu import _ctx, _weights  # noqa: E402
+from frecsys_hip.data import _csr_from_pairs  # noqa: E402
+
+rng = np.random.default_rng(21)
+n_users, n_items = 12000, 40
+hs = [9000, 6150, 4097, 8192, 4100, 2500] + list(rng.integers(40, 600, n_items - 6))
+users = np.concatenate([rng.choice(n_users, int(h), replace=False) for h in hs]).astype(np.int64)
+items = np.concatenate([np.full(int(h), i) for i, h in enumerate(hs)]).astype(np.int64)
+up, uc = _csr_from_pairs(users, items, n_users)
+ip, ic = _csr_from_pairs(items, users, n_items)
+out = {}
+for dim in (512, 1000):
+    ctx, U, V = _ctx(dim, n_users, n_items, up, uc, ip, ic)
+    ctx.gramian(fh.SIDE_USER)
+    ctx.solve_side(fh.SIDE_ITEM, fh.KIND_IALS, 0.003, 0.1)
+    out[f"V{dim}"] = ctx.get_embeddings(fh.SIDE_ITEM)
+np.savez(sys.argv[1], **out)
+print("saved", sys.argv[1])
