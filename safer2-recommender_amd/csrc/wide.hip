@@ -609,15 +609,37 @@ __global__ void __launch_bounds__(512)
 
 #pragma unroll 1
   for (int p = 0; p < T; ++p) {
-    // ---- A: row p of L ----
-    for (int i = tid; i < p * 256; i += 512) {
-      const int q = i >> 8, r = (i >> 3) & 31, c = (i & 7) * 4;
-      const float4 v = *reinterpret_cast<const float4*>(gtile(p, q) + r * 32 + c);
-      float* t = rowL + q * LP + r * 33 + c;
-      t[0] = v.x;
-      t[1] = v.y;
-      t[2] = v.z;
-      t[3] = v.w;
+    // ---- A: row p of L (the thread's loads issued four at a time, each
+    // unconditional -- past the row it re-reads tile (p, 0) and drops it --
+    // so a panel costs two HBM round trips, not one per float4) ----
+    {
+      constexpr int NA = ((T - 1) * 256 + 511) / 512, NB = 4;
+      const int n = p * 256;
+#pragma unroll
+      for (int k0 = 0; k0 < NA; k0 += NB) {
+        if (tid + 512 * k0 < n) {  // wave-uniform (n is a multiple of 256)
+          float4 v[NB];
+#pragma unroll
+          for (int k = 0; k < NB; ++k) {
+            const int i = tid + 512 * (k0 + k);
+            const int ii = i < n ? i : tid;
+            const int q = ii >> 8, r = (ii >> 3) & 31, c = (ii & 7) * 4;
+            v[k] = *reinterpret_cast<const float4*>(gtile(p, q) + r * 32 + c);
+          }
+#pragma unroll
+          for (int k = 0; k < NB; ++k) {
+            const int i = tid + 512 * (k0 + k);
+            if (i < n) {
+              const int q = i >> 8, r = (i >> 3) & 31, c = (i & 7) * 4;
+              float* t = rowL + q * LP + r * 33 + c;
+              t[0] = v[k].x;
+              t[1] = v[k].y;
+              t[2] = v[k].z;
+              t[3] = v[k].w;
+            }
+          }
+        }
+      }
     }
     __syncthreads();
     // ---- B ----
@@ -633,22 +655,25 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
         for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
       }
-      // opaque zero: the swizzled addresses are formed here, not hoisted out
-      // of the panel loop into registers for its whole length
-      int z;
-      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+      // opaque copies of the lane coordinates: the 48 swizzled / padded
+      // addresses below are formed here with a few VALU ops each, not hoisted
+      // out of the panel loop (at 128 registers they were spilled, and every
+      // store of this chain-critical block then waited on a scratch reload)
+      int lo_o, hi_o;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(lo_o) : "v"(lo));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(hi_o) : "v"(hi));
 #pragma unroll
-      for (int q = 0; q < 16; ++q) dinv[sw(acc_row(q, hi), lo) + z] = d[q];
+      for (int q = 0; q < 16; ++q) dinv[sw(acc_row(q, hi_o), lo_o)] = d[q];
       wave_lds_sync();
       if (!diag_factor_inv(dinv, lane) && lane == 0) flag[0] = 1;
       wave_lds_sync();
       float* Aw = gtile(p, p);  // L_pp^-1 for the back substitution, and its padded copy
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int r = 2 * i + hi;
-        const float v = dinv[sw(r, lo) + z];
-        Aw[r * 32 + lo] = v;
-        dpad[r * 33 + lo] = v;
+        const int r = 2 * i + hi_o;
+        const float v = dinv[sw(r, lo_o)];
+        Aw[r * 32 + lo_o] = v;
+        dpad[r * 33 + lo_o] = v;
       }
     } else {
       if (wave == 1) {
