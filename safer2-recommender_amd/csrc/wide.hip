@@ -468,8 +468,24 @@ __global__ void __launch_bounds__(512)
   // kind test compiles into scalar branches per element)
   auto finish = [&](auto mode_c) __attribute__((always_inline)) {
     constexpr int FM = decltype(mode_c)::value;  // 0 iALS, 1 U kinds, 2 V kinds, 3 CVaR
+    // G values one tile ahead: tile m+1's loads are in flight while tile m
+    // is finished and stored (one HBM round trip per epilogue, not one per tile)
+    float gnx[16];
+    auto ldg = [&](int m) __attribute__((always_inline)) {
+      if (tv(m)) {
+        const int I = 8 * BI + tI, J = 8 * BJ + m;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          gnx[q] = a.G[(int64_t)(32 * I + acc_row(q, hi)) * Dp + 32 * J + lo];
+      }
+    };
+    ldg(0);
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
+      float gcur[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) gcur[q] = gnx[q];
+      if (m + 1 < MT) ldg(m + 1);
       if (tv(m)) {
         float* t = otile(m);
         const int I = 8 * BI + tI, J = 8 * BJ + m;
@@ -479,7 +495,7 @@ __global__ void __launch_bounds__(512)
           const int gi = 32 * I + i, gj = 32 * J + lo;
           const bool dg = gi == gj;
           float v = acc[m][q];
-          const float gv = a.G[(int64_t)gi * Dp + gj];
+          const float gv = gcur[q];
           if constexpr (FM == 3) {
             v = assemble(kind, v, gv, dg, a.w, lam, hf, omega);
           } else {
@@ -492,7 +508,7 @@ __global__ void __launch_bounds__(512)
           t[i * 32 + lo] = v;
         }
       }
-      __builtin_amdgcn_sched_barrier(0);  // one tile's G loads live at a time
+      __builtin_amdgcn_sched_barrier(0);  // two tiles' G loads live at a time
     }
   };
   if (grad) finish(std::integral_constant<int, 3>{});
