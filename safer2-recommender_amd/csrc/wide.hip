@@ -419,19 +419,26 @@ __global__ void __launch_bounds__(512)
   if (MODE == 1 && fin) {
     // the unsplit kernel's two-level sum: block sums folded left to right
     // (t = s_1, t = t + s_j, ..., s_last + t), b likewise from 0
+    // (the next tile's slab values in flight under each add, across slabs)
     const int2 sp = a.split[pos0 + unit];
+    f32x16 nx;
+    auto lds_ = [&](int j, int m) __attribute__((always_inline)) {
+      if (j < sp.y && tv(m)) {
+        const float* t = stile(a.slabs + (size_t)(sp.x + j) * slab_floats, m);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) nx[q] = t[q * 64];
+      }
+    };
+    lds_(0, 0);
 #pragma unroll 1
     for (int j = 0; j < sp.y; ++j) {
       const float* sb = a.slabs + (size_t)(sp.x + j) * slab_floats;
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        if (tv(m)) {
-          const float* t = stile(sb, m);
-          f32x16 v;
-#pragma unroll
-          for (int q = 0; q < 16; ++q) v[q] = t[q * 64];
-          acc[m] = j == 0 ? v : acc[m] + v;
-        }
+        const f32x16 v = nx;
+        if (m + 1 < MT) lds_(j, m + 1);
+        else lds_(j + 1, 0);
+        if (tv(m)) acc[m] = j == 0 ? v : acc[m] + v;
         __builtin_amdgcn_sched_barrier(0);
       }
       if (bown) {
