@@ -168,6 +168,29 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
       }
     }
   };
+  // the same in two halves for the BF loop: the id load issued ahead of the
+  // chunk's row gathers, the (dependent) weights formed at the end of the
+  // step -- a use of the id right after the gathers would wait (in-order
+  // vmcnt) for those rows too, stalling wave 0 a full HBM latency per chunk
+  auto ring_id_load = [&](int c) {
+    const int64_t k = k0 + (int64_t)c * R + tid;
+    return k < k1 ? a.col[p0 + virt_pos(k, h)] : -1;
+  };
+  auto ring_weights = [&](int c, int id, float& sa, float& bw) {
+    const int64_t k = k0 + (int64_t)c * R + tid;
+    sa = 0.0f;
+    bw = 0.0f;
+    if (k < k1) {
+      if (vk) {
+        const float nu = a.other_weight[id];
+        sa = sqrtf(nu);
+        bw = (k < h && sa > 0.0f) ? nu / sa : 0.0f;
+      } else {
+        sa = 1.0f;
+        bw = 1.0f;
+      }
+    }
+  };
   auto ring_store = [&](int c, int id, float sa, float bw) {
     const int s = (c % kRing) * R + tid;
     ring_id[s] = id;
@@ -387,11 +410,14 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     lds_barrier();
     auto step = [&](int c, float (&xcur)[16], float (&xnxt)[16]) {
       const int buf = c & 1;
-      if (c + 2 < nchunks) load_bf(c + 2, xnxt);
       const bool ring_more = (tid < R) && (c + 3 < nchunks);
       int nid = -1;
-      float nsa = 0.f, nbw = 0.f;
-      if (ring_more) ring_load(c + 3, nid, nsa, nbw);
+      if (ring_more) nid = ring_id_load(c + 3);
+      // unconditional (past the end it re-gathers the last chunk, whose ring
+      // slot stays valid; the values are never staged): a conditional load
+      // block here made the waitcnt pass wait (vmcnt) for these fresh rows
+      // before this step's scaling and MFMAs
+      load_bf(c + 2 < nchunks ? c + 2 : nchunks - 1, xnxt);
       const bool live = c + 1 < nchunks;
       // chunk c+1's staging math is spread over the issue gaps of this
       // chunk's MFMAs: scaled values (and the rhs part) first, then two
@@ -446,7 +472,11 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
         for (int k = 0; k < SLOTS; ++k) split_slot(k);
       }
       if (live) write_bf(buf ^ 1, f);
-      if (ring_more) ring_store(c + 3, nid, nsa, nbw);
+      if (ring_more) {
+        float nsa, nbw;
+        ring_weights(c + 3, nid, nsa, nbw);
+        ring_store(c + 3, nid, nsa, nbw);
+      }
       lds_barrier();
     };
     for (int c = 0; c < nchunks; c += 2) {

@@ -378,8 +378,16 @@ __global__ void __launch_bounds__(512)
         __builtin_amdgcn_sched_barrier(0);
       }
       if ((c + 1) % W2FLUSH == 0 && more) flush();  // block-uniform
-      if (more && c + 2 < nchunks) load(c + 2);
+      // the ring slot first: its store waits (vmcnt) for the ring loads, and
+      // placed after load(c+2) that wait -- in-order counters, a conditional
+      // load between -- was vmcnt(0), wave 0 stalling on the rows it had just
+      // requested (a full HBM latency per chunk, every wave behind it at the
+      // barrier)
       if (ring_more) ring_store(c + 3, nid, nsa, nbw);
+      // unconditional (past the end it re-gathers the last chunk, whose ring
+      // slot stays valid; never staged): a conditional load here made the
+      // waitcnt pass flush vmcnt at the loop head, stalling on these rows
+      load(c + 2 < nchunks ? c + 2 : nchunks - 1);
       lds_barrier();
     }
   };

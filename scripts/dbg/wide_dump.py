@@ -21,7 +21,7 @@ items = np.concatenate([np.full(int(h), i) for i, h in enumerate(hs)]).astype(np
 up, uc = _csr_from_pairs(users, items, n_users)
 ip, ic = _csr_from_pairs(items, users, n_items)
 out = {}
-for dim in (512, 1000):
+for dim in (128, 256, 512, 1000):
     ctx, U, V = _ctx(dim, n_users, n_items, up, uc, ip, ic)
     ctx.gramian(fh.SIDE_USER)
     ctx.solve_side(fh.SIDE_ITEM, fh.KIND_IALS, 0.003, 0.1)
