@@ -231,16 +231,17 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   // two register sets and two LDS stages: slab c+2's loads are issued when
   // slab c starts and stored at the end of slab c+1 (two slabs of cover)
   float4 ra[NQ], rb[NQ];
+  // the padding rows (id < 0) load row 0 and are zeroed where they are
+  // stored: a conditional load with a zero default made the waitcnt pass
+  // wait (vmcnt) for the fresh slab at the loop head and mid-slab
   auto load_slab = [&](int c, float4 (&regs)[NQ]) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int s = tid + q * NTHR;
-      regs[q] = make_float4(0.f, 0.f, 0.f, 0.f);
       if ((HP * 8) % NTHR == 0 || s < HP * 8) {
         const int r = s >> 3, c4 = s & 7;
-        const int id = ids[r];
-        if (id >= 0 && !FRECSYS_SKIP(a.debug_skip, 32))
-          regs[q] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)id * Dp + 32 * c + 4 * c4);
+        const int id = max(ids[r], 0);
+        regs[q] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)id * Dp + 32 * c + 4 * c4);
       }
     }
   };
@@ -250,11 +251,12 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
       const int s = tid + q * NTHR;
       if ((HP * 8) % NTHR == 0 || s < HP * 8) {
         const int r = s >> 3, c4 = s & 7;
+        const bool ok = ids[r] >= 0 && !FRECSYS_SKIP(a.debug_skip, 32);
         float* d = stage + (buf % C::NSTAGE) * C::STG + r * SROW + 4 * c4;
-        d[0] = regs[q].x;
-        d[1] = regs[q].y;
-        d[2] = regs[q].z;
-        d[3] = regs[q].w;
+        d[0] = ok ? regs[q].x : 0.0f;
+        d[1] = ok ? regs[q].y : 0.0f;
+        d[2] = ok ? regs[q].z : 0.0f;
+        d[3] = ok ? regs[q].w : 0.0f;
       }
     }
   };
