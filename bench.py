@@ -152,7 +152,7 @@ def path_accounting(ctx, spec, ptrs, timers, K):
     d = spec["dim"]
     Dp = fh.padded_dim(d)
     wide = Dp > 256
-    dual_max, split_rows = ctx.history_space_max_h(), 1024
+    dual_max, split_rows = ctx.history_space_max_h(), 4096  # capi.hip split_rows default
     chol = d ** 3 / 3.0 + 2.0 * d * d
     fin_flops, fin_ms, fin_n = 0.0, 0.0, 0
     paths = {}

@@ -120,7 +120,7 @@ struct frecsys_ctx {
   size_t cap_wide_ws = 0;
   int64_t wide_ws_mb = 4096;     // FRECSYS_WIDE_WS_MB: workspace budget
   // long-history split of the d-space solve
-  int split_rows = 1024;         // rows per partial SYRK (FRECSYS_SPLIT_ROWS, 0 = off)
+  int split_rows = 4096;         // rows per partial SYRK (FRECSYS_SPLIT_ROWS, 0 = off; swept 512..4096 at ML-20M d=256: 4096 best)
   std::vector<int2> h_split;
   std::vector<SplitWork> h_work;
   int2* d_split = nullptr;
