@@ -60,7 +60,8 @@ $(MODELDUMP): tests/cpp/model_dump.cc $(FRECSYS_HDRS) include/frecsys_hip.h $(LI
 	    -Wl,-rpath,'$$ORIGIN/../frecsys_hip'
 
 # Profiling-only build with the FRECSYS_DEBUG_SKIP ablation masks compiled in
-# (the shipped library refuses the variable).  scripts/ab_bench.sh swaps it in.
+# (the shipped library refuses the variable); LD_LIBRARY_PATH / a copy over
+# frecsys_hip/libfrecsys_hip.so swaps it in for an ablation run.
 ABL_LIB := ab/libfrecsys_hip_ablation.so
 ablation: $(ABL_LIB)
 $(ABL_LIB): $(HIP_SRCS) $(HDRS)

@@ -51,8 +51,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "safer2-recommender_amd"))
 
-import frecsys_hip as fh  # noqa: E402
-from frecsys_hip.data import SHAPES, synthetic  # noqa: E402
+# frecsys_hip is imported in main(), after the launcher decision: a parent
+# that spawns the N ranks must not have touched the GPU library.
+fh = None
+SHAPES = synthetic = None
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (spec)
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -93,7 +95,42 @@ def parse():
     ap.add_argument("--allow-env", action="store_true",
                     help="run although FRECSYS_* variables are set (recorded in the line)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--print-launch", action="store_true",
+                    help="print the N-rank launch command bench.py would run and exit")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(args):
+    """One process per GPU: torch.distributed.run on this node, rendezvous on
+    127.0.0.1, the same bench.py arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+            f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+
+
+def world_from_env(args):
+    """(world, rank, local_rank) of this process, or None when bench.py must
+    launch the ranks itself (--gpus N > 1 without a torchrun environment).
+    Exits non-zero when the environment's world size is not --gpus."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            return None
+        env_world = "1"
+    world = int(env_world)
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+                 f"{world}-rank run as {args.gpus} GPUs")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
 
 
 def log(msg, rank=0):
@@ -272,6 +309,10 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
                      comm_id=cid, **spec["flags"])
     del users
     ctx = model.context()
+    cw, _, comm_ranks = ctx.comm_world()
+    if world > 1 and (cw != world or comm_ranks != world):
+        raise SystemExit(f"bench.py: the model joined world {cw} with an RCCL communicator of "
+                         f"{comm_ranks} ranks, expected {world}")
     model.initialize()  # run_model.cc:246-257 (SAFER2); outside the timed region
 
     def barrier():
@@ -320,6 +361,7 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
         "baseline_config": f"BASELINE.json configs[{spec['config']}]",
         "model": spec["model"], "flags": spec["flags"], "flags_source": spec["readme"],
         "n_users": nu, "n_items": ni, "nnz": nnz, "dim": d, "padded_dim": Dp,
+        "rccl_ranks": comm_ranks,
         "value": nu * K / elapsed, "unit": "user-solve updates/s",
         "steps": K, "warmup": warmup,
         "ms_per_step": elapsed / K * 1e3, "sec_per_epoch": elapsed / K,
@@ -363,14 +405,28 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
 
 
 def main():
+    global fh, SHAPES, synthetic
     args = parse()
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
     env = frecsys_env()
     if env and not args.allow_env:
         sys.exit(f"bench.py: refusing to run with {sorted(env)} set (profiling path selectors; "
                  f"pass --allow-env to run anyway, recorded in the line)")
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ranks = world_from_env(args)
+    if ranks is None:  # launch the N ranks (children) and exit with their status
+        cmd = launch_command(args)
+        if args.print_launch:
+            print(json.dumps(cmd))
+            return
+        sys.exit(subprocess.run(cmd).returncode)
+    if args.print_launch:
+        print(json.dumps(None))
+        return
+    world, rank, local_rank = ranks
+    import frecsys_hip as fh_mod
+    from frecsys_hip import data as fh_data
+    fh, SHAPES, synthetic = fh_mod, fh_data.SHAPES, fh_data.synthetic
     dist = None
     if world > 1:
         import torch
@@ -395,6 +451,7 @@ def main():
             "value": head["value"],
             "unit": "user-solve updates/s",
             "n_gpus": world,
+            "rccl_ranks": head["rccl_ranks"],
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": head["ms_per_step"],

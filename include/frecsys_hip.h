@@ -117,6 +117,13 @@ int32_t frecsys_padded_dim(int32_t dim);
  * bounds[0]=0 .. bounds[nparts]=n_rows (safe to call without a GPU). */
 int frecsys_partition(int64_t n_rows, const int64_t* row_ptr, int32_t nparts,
                       int64_t* bounds);
+/* Host-only: the partition-independent Gramian plan of n_rows rows at
+ * `dim` (frecsys_gramian): rows per leaf, leaves, groups (group g = leaves
+ * [g*n_leaves/n_groups, (g+1)*n_leaves/n_groups)) and the groups
+ * [own_lo, own_hi) rank `rank` of `world` computes.  Any output may be NULL. */
+int frecsys_gram_plan(int32_t dim, int64_t n_rows, int32_t world, int32_t rank,
+                      int64_t* rows_per_leaf, int64_t* n_leaves, int32_t* n_groups,
+                      int32_t* own_lo, int32_t* own_hi);
 /* RCCL unique id (128 bytes) -- call on rank 0, broadcast to the others. */
 int frecsys_comm_unique_id(uint8_t id[128]);
 /* Join rank `rank` of `world`.  id != NULL: RCCL communicator; the library
@@ -129,6 +136,10 @@ int frecsys_comm_unique_id(uint8_t id[128]);
  * process sharing a device. */
 int frecsys_comm_init(frecsys_ctx* ctx, int32_t world, int32_t rank,
                       const uint8_t id[128]);
+/* World size and rank the context joined, and the rank count of its RCCL
+ * communicator (ncclCommCount; 0 without one). */
+int frecsys_comm_world(const frecsys_ctx* ctx, int32_t* world, int32_t* rank,
+                       int32_t* comm_ranks);
 /* Row range [lo, hi) of `side` owned by this rank (after load_csr). */
 int frecsys_shard_range(const frecsys_ctx* ctx, int32_t side, int64_t* lo,
                         int64_t* hi);
@@ -148,10 +159,32 @@ int frecsys_snapshot(frecsys_ctx* ctx, int32_t side);
 
 /* ---- compute ---- */
 /* G[side] = X^T diag(w) X over all rows of side's embeddings (or of its
- * snapshot); each rank sums its shard, then RCCL all-reduce.  weights: host
- * [rows of side] or NULL.  host_out (dim x dim, row-major) may be NULL. */
+ * snapshot).  Partition-independent: the rows are cut into fixed leaves and
+ * the leaves into n_groups fixed groups (frecsys_gram_groups; the cut depends
+ * only on the row count); each rank computes the slabs of its own groups,
+ * the slabs are all-gathered over RCCL and every rank sums them in group
+ * order, so G is bitwise the same at every world size.  Without a
+ * communicator at world > 1 (external exchange) G is the sum of this rank's
+ * groups only; the caller exchanges the group slabs (frecsys_get_gram_groups
+ * / frecsys_set_gram_groups) or partial Gramians (frecsys_set_gramian).
+ * weights: host [rows of side] or NULL.  host_out (dim x dim, row-major) may
+ * be NULL. */
 int frecsys_gramian(frecsys_ctx* ctx, int32_t side, const float* weights,
                     int32_t from_snapshot, float* host_out);
+/* Read G[side] as the context holds it (dim x dim, leading dim ld). */
+int frecsys_get_gramian(frecsys_ctx* ctx, int32_t side, float* host, int64_t ld);
+/* The Gramian plan of `side`: group count, the groups [own_lo, own_hi) this
+ * rank computes, floats per group slab (any pointer may be NULL). */
+int frecsys_gram_groups(const frecsys_ctx* ctx, int32_t side, int32_t* n_groups,
+                        int32_t* own_lo, int32_t* own_hi, int64_t* floats_per_group);
+/* All group slabs of the last Gramian of `side` formed here (host
+ * [n_groups * floats_per_group]; at world > 1 without a communicator, the
+ * other ranks' slabs are zero). */
+int frecsys_get_gram_groups(frecsys_ctx* ctx, int32_t side, float* host);
+/* G[side] = the group-order sum of the given slabs (every group's slab, as
+ * gathered from the owners): the external-exchange completion of
+ * frecsys_gramian. */
+int frecsys_set_gram_groups(frecsys_ctx* ctx, int32_t side, const float* host);
 /* Overwrite G[side] with a host dim x dim matrix (row-major, leading dim
  * ld) -- the static Project* entry points take an arbitrary Gramian. */
 int frecsys_set_gramian(frecsys_ctx* ctx, int32_t side, const float* host,

@@ -73,6 +73,14 @@ int frecsys_model_train(frecsys_model* m, int32_t epochs);
 frecsys_ctx* frecsys_model_context(frecsys_model* m);
 /* GetMeanWeight() of SAFER2 / SAFER2++ (safer2.h:815-817); alpha for ERM-MF. */
 float frecsys_model_mean_weight(const frecsys_model* m);
+/* The dual state of ERM-MF / CVaR-MF / SAFER2 (-MF++): weights[n_users] =
+ * the omega the last Train() (or Initialize()) left -- the weights its
+ * half-steps used (safer2.h:272-290) --, losses[n_users] = user_loss_ of the
+ * last ComputeUserLoss, item_reg[n_items] = item_reg_ (safer2.h:831-837),
+ * xi = the current xi (SAFER2 / SAFER2++; NaN otherwise).  Any pointer may be
+ * NULL; iALS has none of these (FRECSYS_ERR_INVALID for weights/item_reg). */
+int frecsys_model_dual_state(const frecsys_model* m, float* weights, float* losses,
+                             float* item_reg, float* xi);
 void frecsys_model_destroy(frecsys_model* m);
 const char* frecsys_model_last_error(void);
 

@@ -237,14 +237,22 @@ static void add_lower(float* A, const float* T, int d) {
 }
 
 /* LLT<MatrixXf, Lower> (ials.h:140): reads the lower triangle only.
- * Every element sees the arithmetic of the left-looking dot-product form of
- * Eigen's unblocked kernel (Eigen/src/Cholesky/LLT.h llt_inplace::unblocked):
- * L(i,j) = (A(i,j) - L(i,0)L(j,0) - L(i,1)L(j,1) - ...) / L(j,j), the
- * subtractions in ascending k, no FMA contraction (-std=c11).  It is run
- * right-looking -- column j's products are subtracted from the trailing
- * lower triangle as soon as column j is final -- which performs the same
- * subtractions in the same order per element (bit-identical results) with
- * a unit-stride inner loop the compiler vectorises.  L overwrites lower. */
+ * The formulas are those of Eigen 3.4's llt_inplace::unblocked
+ * (Eigen/src/Cholesky/LLT.h): L(i,j) = (A(i,j) - sum_k<j L(i,k)L(j,k)) /
+ * L(j,j), L(j,j) = sqrt(A(j,j) - sum_k<j L(j,k)^2), each sum formed here
+ * sequentially in ascending k, no FMA contraction (-std=c11).  This is NOT
+ * Eigen's summation order: LLT::compute calls llt_inplace::blocked, which
+ * runs the unblocked kernel only below size 32 and otherwise factors panels
+ * of clamp((d/8)/16*16, 8, 128) columns with a TRSM and a rankUpdate of the
+ * trailing block, and its squaredNorm / GEMV reductions are packet-
+ * vectorised (an order that depends on the SIMD width of the reference's
+ * build).  The two orders agree to fp32 rounding, far inside the 1e-4 bar;
+ * element-wise parity with Eigen itself stays unpinned (Eigen is absent,
+ * SURVEY 8(c)).  Run right-looking -- column j's products are subtracted
+ * from the trailing lower triangle as soon as column j is final -- which
+ * performs the same subtractions in the same order per element as the
+ * ascending-k dot-product form (bit-identical results) with a unit-stride
+ * inner loop the compiler vectorises.  L overwrites lower. */
 static int cholesky_lower(float* A, int d) {
   float* c = (float*)malloc(sizeof(float) * (size_t)(d > 0 ? d : 1));
   int rc = 0;

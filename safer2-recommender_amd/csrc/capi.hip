@@ -21,6 +21,7 @@
 #include <map>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/frecsys_hip.h"
@@ -61,8 +62,12 @@ struct frecsys_ctx {
   size_t cap_other_weight = 0;
   float* d_gram_w = nullptr;
   size_t cap_gram_w = 0;
-  float* d_partials = nullptr;
+  float* d_partials = nullptr;   // Gramian leaf workspace
   size_t cap_partials = 0;
+  float* d_gslabs[3] = {nullptr, nullptr, nullptr};  // Gramian group slabs per side (2: train stats)
+  size_t cap_gslabs[3] = {0, 0, 0};
+  GramPlan gplan[2];             // plan of the last Gramian formed per side
+  int gram_own[2][2] = {{0, 0}, {0, 0}};  // ... and the groups this rank computed
   float* d_loss = nullptr;
   size_t cap_loss = 0;
   float* d_quad = nullptr;
@@ -118,7 +123,10 @@ struct frecsys_ctx {
   size_t cap_topk = 0;
   float* wide_ws = nullptr;      // [wide batch][wide_slot_floats(Dp)]
   size_t cap_wide_ws = 0;
-  int64_t wide_ws_mb = 4096;     // FRECSYS_WIDE_WS_MB: workspace budget
+  // FRECSYS_WIDE_WS_MB: the budget of EACH of the two wide d-space buffers
+  // (the batch workspace of A tiles, and the long-history slabs): up to
+  // twice this in device memory (8 GB of 288 at the default)
+  int64_t wide_ws_mb = 4096;
   // long-history split of the d-space solve
   int split_rows = 4096;         // rows per partial SYRK (FRECSYS_SPLIT_ROWS, 0 = off; swept 512..4096 at ML-20M d=256: 4096 best)
   std::vector<int2> h_split;
@@ -482,6 +490,66 @@ void flush_ktimers(frecsys_ctx* c) {
   c->pending.clear();
 }
 
+// Group slabs of [r's groups] broadcast from their owners (an all-gather
+// with uneven counts, in place).
+int allgather_groups(frecsys_ctx* c, float* gslabs, const GramPlan& pl) {
+  if (!c->comm || pl.ngroup == 0) return FRECSYS_OK;
+  NCCL_TRY(c, ncclGroupStart());
+  for (int r = 0; r < c->world; ++r) {
+    int lo, hi;
+    gram_owned_groups(pl, c->world, r, &lo, &hi);
+    if (hi <= lo) continue;
+    float* p = gslabs + (size_t)lo * pl.slab_floats;
+    NCCL_TRY(c, ncclBroadcast(p, p, (size_t)(hi - lo) * pl.slab_floats, ncclFloat, r, c->comm,
+                              c->stream));
+  }
+  NCCL_TRY(c, ncclGroupEnd());
+  return FRECSYS_OK;
+}
+
+// G = X^T diag(w) X over all rows of X (n rows) by the partition-
+// independent plan (kernels.h GramPlan): this rank computes its own groups,
+// the group slabs are all-gathered (with a communicator) and every rank sums
+// them in group order.  Without a communicator at world > 1 (external
+// exchange) the other ranks' slabs are zero: G is this rank's partial sum.
+// `all_groups`: compute every group here (diagnostics on one rank).
+int form_gramian(frecsys_ctx* c, int slot, const float* X, int64_t n, const float* dw, float* G,
+                 bool all_groups) {
+  const GramPlan pl = gram_plan(c->Dp, n);
+  int g_lo = 0, g_hi = pl.ngroup;
+  if (!all_groups) gram_owned_groups(pl, c->world, c->rank, &g_lo, &g_hi);
+  int rc = ensure(c, &c->d_partials, &c->cap_partials, gram_leaf_floats(pl, g_lo, g_hi));
+  if (rc) return rc;
+  rc = ensure(c, &c->d_gslabs[slot], &c->cap_gslabs[slot],
+              std::max<size_t>((size_t)pl.ngroup * pl.slab_floats, 1));
+  if (rc) return rc;
+  if (!all_groups && c->world > 1 && !c->comm && pl.ngroup > 0)
+    HIP_TRY(c, hipMemsetAsync(c->d_gslabs[slot], 0, sizeof(float) * pl.ngroup * pl.slab_floats,
+                              c->stream));
+  GramArgs g{};
+  g.X = X;
+  g.w = dw;
+  g.partials = c->d_partials;
+  g.gslabs = c->d_gslabs[slot];
+  g.plan = pl;
+  g.g_lo = g_lo;
+  g.g_hi = g_hi;
+  HIP_TRY(c, launch_gramian(c->Dp, g, c->stream));
+  if (!all_groups && c->comm) {
+    const size_t k = ktimer_begin(c, "gram_exchange", c->stream);
+    rc = allgather_groups(c, c->d_gslabs[slot], pl);
+    if (rc) return rc;
+    ktimer_end(c, k, c->stream);
+  }
+  HIP_TRY(c, launch_gram_final(c->Dp, pl, c->d_gslabs[slot], G, c->stream));
+  if (slot < 2) {
+    c->gplan[slot] = pl;
+    c->gram_own[slot][0] = g_lo;
+    c->gram_own[slot][1] = g_hi;
+  }
+  return FRECSYS_OK;
+}
+
 // Restatement of libstdc++ std::normal_distribution<float>::operator()
 // (Marsaglia polar; bits/random.tcc) over std::generate_canonical<float,24>
 // of std::mt19937, with FMA contraction off so x*x + y*y rounds like the
@@ -517,6 +585,48 @@ struct NormalF {
     return ret * stddev + mean;
   }
 };
+
+// n draws of a fresh NormalF (a new distribution per matrix,
+// recommender.h:61-67) from g, bit-identical to calling it n times, in two
+// passes: the polar method's accept / reject decisions need only the
+// uniforms (a cheap sequential scan that advances g exactly as NormalF
+// does), and the log / sqrt of each accepted pair are independent, so they
+// run on threads.  2M x 1024 + 500K x 1024 draws: the serial loop's ~1 min
+// becomes a few seconds.
+void fill_normal(std::mt19937& g, float mean, float stddev, float* out, size_t n) {
+  const size_t pairs = (n + 1) / 2;
+  std::vector<float> px(pairs), py(pairs), pr(pairs);
+  for (size_t p = 0; p < pairs; ++p) {
+    float x, y, r2;
+    do {
+      x = (float)((double)(2.0f * NormalF::canonical(g)) - 1.0);
+      y = (float)((double)(2.0f * NormalF::canonical(g)) - 1.0);
+      r2 = x * x + y * y;
+    } while (r2 > 1.0 || r2 == 0.0);
+    px[p] = x;
+    py[p] = y;
+    pr[p] = r2;
+  }
+  auto work = [&](size_t lo, size_t hi) {
+    for (size_t p = lo; p < hi; ++p) {
+      const float r2 = pr[p];
+      const float mult = std::sqrt(-2 * std::log(r2) / r2);
+      const float first = py[p] * mult;   // returned first ...
+      const float second = px[p] * mult;  // ... then the saved value
+      out[2 * p] = first * stddev + mean;
+      if (2 * p + 1 < n) out[2 * p + 1] = second * stddev + mean;
+    }
+  };
+  const size_t nt = std::min<size_t>(16, std::max(1u, std::thread::hardware_concurrency()));
+  if (pairs < (size_t)1 << 16 || nt == 1) {
+    work(0, pairs);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back(work, pairs * t / nt, pairs * (t + 1) / nt);
+  for (auto& t : th) t.join();
+}
 #pragma clang fp contract(on)
 
 }  // namespace
@@ -546,6 +656,23 @@ int frecsys_partition(int64_t n_rows, const int64_t* row_ptr, int32_t nparts, in
   if (n_rows < 0 || nparts <= 0 || !row_ptr || !bounds)
     return fail(nullptr, FRECSYS_ERR_INVALID, "frecsys_partition: bad arguments");
   partition_rows(n_rows, row_ptr, nparts, bounds);
+  return FRECSYS_OK;
+}
+
+int frecsys_gram_plan(int32_t dim, int64_t n_rows, int32_t world, int32_t rank,
+                      int64_t* rows_per_leaf, int64_t* n_leaves, int32_t* n_groups,
+                      int32_t* own_lo, int32_t* own_hi) {
+  const int Dp = padded_dim(dim);
+  if (Dp == 0 || n_rows < 0 || world <= 0 || rank < 0 || rank >= world)
+    return fail(nullptr, FRECSYS_ERR_INVALID, "frecsys_gram_plan: bad arguments");
+  const GramPlan pl = gram_plan(Dp, n_rows);
+  int lo, hi;
+  gram_owned_groups(pl, world, rank, &lo, &hi);
+  if (rows_per_leaf) *rows_per_leaf = pl.rpl;
+  if (n_leaves) *n_leaves = pl.nleaf;
+  if (n_groups) *n_groups = pl.ngroup;
+  if (own_lo) *own_lo = lo;
+  if (own_hi) *own_hi = hi;
   return FRECSYS_OK;
 }
 
@@ -657,7 +784,8 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
     if (c->gram[s]) (void)hipFree(c->gram[s]);
   }
   for (float* p : {c->d_entity_weight, c->d_entity_reg, c->d_other_weight, c->d_gram_w,
-                   c->d_partials, c->d_loss, c->d_quad})
+                   c->d_partials, c->d_loss, c->d_quad, c->d_gslabs[0], c->d_gslabs[1],
+                   c->d_gslabs[2]})
     if (p) (void)hipFree(p);
   if (c->d_fail) (void)hipFree(c->d_fail);
   if (c->d_counter) (void)hipFree(c->d_counter);
@@ -847,9 +975,8 @@ int frecsys_init_embeddings(frecsys_ctx* c, uint32_t seed, float stdev) {
   std::mt19937 gen{seed};
   const float adjusted = (float)((double)stdev / std::sqrt((double)c->dim));
   for (int s = 0; s < 2; ++s) {
-    NormalF d;
     std::vector<float> h((size_t)c->n[s] * c->dim);
-    for (auto& v : h) v = d(gen, 0.0f, adjusted);
+    fill_normal(gen, 0.0f, adjusted, h.data(), h.size());
     if (c->n[s]) {
       int rc = frecsys_set_embeddings(c, s, h.data(), c->dim);
       if (rc) return rc;
@@ -891,33 +1018,17 @@ int frecsys_gramian(frecsys_ctx* c, int32_t side, const float* weights, int32_t 
   }
   rc = join_eager(c, 1 << side, c->stream);  // an early basis build still reading this G
   if (rc) return rc;
-  int64_t lo, hi;
-  shard(c, side, &lo, &hi);
-  const int64_t rows = hi - lo;
   const float* dw = nullptr;
   if (weights) {
     rc = upload(c, &c->d_gram_w, &c->cap_gram_w, weights, (size_t)c->n[side]);
     if (rc) return rc;
     dw = c->d_gram_w;
   }
-  rc = ensure(c, &c->d_partials, &c->cap_partials, gram_workspace_floats(c->Dp, rows));
-  if (rc) return rc;
-  GramArgs g;
-  g.X = from_snapshot ? c->snap[side] : c->emb[side];
-  g.row0 = lo;
-  g.n = rows;
-  g.w = dw;
-  g.partials = c->d_partials;
-  g.G = c->gram[side];
   {
     ScopedTimer t(c, "gramian");
-    HIP_TRY(c, launch_gramian(c->Dp, g, c->stream));
-    t.stop();
-  }
-  if (c->comm) {
-    ScopedTimer t(c, "allreduce");
-    NCCL_TRY(c, ncclAllReduce(c->gram[side], c->gram[side], (size_t)c->Dp * c->Dp, ncclFloat,
-                              ncclSum, c->comm, c->stream));
+    rc = form_gramian(c, side, from_snapshot ? c->snap[side] : c->emb[side], c->n[side], dw,
+                      c->gram[side], false);
+    if (rc) return rc;
     t.stop();
   }
   c->gram_ver[side] = ++c->ver_counter;
@@ -929,6 +1040,77 @@ int frecsys_gramian(frecsys_ctx* c, int32_t side, const float* weights, int32_t 
   rc = maybe_start_eager(c, side);
   if (rc) return rc;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  flush_ktimers(c);
+  return FRECSYS_OK;
+}
+
+int frecsys_get_gramian(frecsys_ctx* c, int32_t side, float* host, int64_t ld) {
+  if (!c || side < 0 || side > 1 || !host || ld < c->dim)
+    return fail(c, FRECSYS_ERR_INVALID, "get_gramian: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipMemcpy2DAsync(host, sizeof(float) * ld, c->gram[side], sizeof(float) * c->Dp,
+                              sizeof(float) * c->dim, c->dim, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_gram_groups(const frecsys_ctx* c, int32_t side, int32_t* n_groups, int32_t* own_lo,
+                        int32_t* own_hi, int64_t* floats_per_group) {
+  if (!c || side < 0 || side > 1) return FRECSYS_ERR_INVALID;
+  const GramPlan pl = gram_plan(c->Dp, c->n[side]);
+  int lo, hi;
+  gram_owned_groups(pl, c->world, c->rank, &lo, &hi);
+  if (n_groups) *n_groups = pl.ngroup;
+  if (own_lo) *own_lo = lo;
+  if (own_hi) *own_hi = hi;
+  if (floats_per_group) *floats_per_group = (int64_t)pl.slab_floats;
+  return FRECSYS_OK;
+}
+
+int frecsys_get_gram_groups(frecsys_ctx* c, int32_t side, float* host) {
+  if (!c || side < 0 || side > 1 || !host)
+    return fail(c, FRECSYS_ERR_INVALID, "get_gram_groups: bad arguments");
+  const GramPlan& pl = c->gplan[side];
+  if (!c->d_gslabs[side] || pl.n != c->n[side])
+    return fail(c, FRECSYS_ERR_INVALID, "get_gram_groups: no Gramian formed for side");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (pl.ngroup)
+    HIP_TRY(c, hipMemcpyAsync(host, c->d_gslabs[side], sizeof(float) * pl.ngroup * pl.slab_floats,
+                              hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_set_gram_groups(frecsys_ctx* c, int32_t side, const float* host) {
+  if (!c || side < 0 || side > 1 || !host)
+    return fail(c, FRECSYS_ERR_INVALID, "set_gram_groups: bad arguments");
+  HIP_TRY(c, hipSetDevice(c->device));
+  int rc = join_eager(c, 1 << side, c->stream);
+  if (rc) return rc;
+  const GramPlan pl = gram_plan(c->Dp, c->n[side]);
+  rc = ensure(c, &c->d_gslabs[side], &c->cap_gslabs[side],
+              std::max<size_t>((size_t)pl.ngroup * pl.slab_floats, 1));
+  if (rc) return rc;
+  if (pl.ngroup)
+    HIP_TRY(c, hipMemcpyAsync(c->d_gslabs[side], host, sizeof(float) * pl.ngroup * pl.slab_floats,
+                              hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_gram_final(c->Dp, pl, c->d_gslabs[side], c->gram[side], c->stream));
+  c->gplan[side] = pl;
+  c->gram_ver[side] = ++c->ver_counter;
+  c->gram_src[side] = 0;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_comm_world(const frecsys_ctx* c, int32_t* world, int32_t* rank, int32_t* comm_ranks) {
+  if (!c) return FRECSYS_ERR_INVALID;
+  if (world) *world = c->world;
+  if (rank) *rank = c->rank;
+  if (comm_ranks) {
+    int n = 0;
+    if (c->comm && ncclCommCount(c->comm, &n) != ncclSuccess) return FRECSYS_ERR_RCCL;
+    *comm_ranks = n;  // 0: no communicator
+  }
   return FRECSYS_OK;
 }
 
@@ -962,7 +1144,7 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
     const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(ap.n_rows, budget));
     int rc = ensure(c, &c->wide_ws, &c->cap_wide_ws, (size_t)batch * slot);
     if (rc) return rc;
-    if (can_split) {  // long histories of the first batch cut into slabs (same budget)
+    if (can_split) {  // long histories of the first batch cut into slabs (a budget of their own)
       const size_t sf = wide_slab_floats(c->Dp);
       rc = plan_split(c, hs, batch, heff, &ap, wide_slab_rows(), sf,
                       (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (sf * sizeof(float))));
@@ -1515,20 +1697,11 @@ int frecsys_train_stats(frecsys_ctx* c, double* observed, double* unobserved,
   if (unobserved) {
     rc = ensure(c, &c->d_gstat, &c->cap_gstat, (size_t)2 * Dp * Dp);
     if (rc) return rc;
-    rc = ensure(c, &c->d_partials, &c->cap_partials,
-                gram_workspace_floats(Dp, std::max<int64_t>(std::max(nu, ni), 1)));
-    if (rc) return rc;
     rc = ensure(c, &c->d_dot, &c->cap_dot, 1);
     if (rc) return rc;
     for (int s = 0; s < 2; ++s) {
-      GramArgs g{};
-      g.X = c->emb[s];
-      g.row0 = 0;
-      g.n = c->n[s];
-      g.w = nullptr;
-      g.partials = c->d_partials;
-      g.G = c->d_gstat + (size_t)s * Dp * Dp;
-      HIP_TRY(c, launch_gramian(Dp, g, c->stream));
+      rc = form_gramian(c, 2, c->emb[s], c->n[s], nullptr, c->d_gstat + (size_t)s * Dp * Dp, true);
+      if (rc) return rc;
     }
     HIP_TRY(c, launch_gram_dot(c->d_gstat, c->d_gstat + (size_t)Dp * Dp, Dp, c->d_dot, c->stream));
     HIP_TRY(c, hipMemcpyAsync(unobserved, c->d_dot, sizeof(double), hipMemcpyDeviceToHost,

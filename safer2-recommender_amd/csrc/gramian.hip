@@ -5,10 +5,14 @@
 // (safer2.h:504-509).  Dense and regular, so it is the one MFMA-shaped op of
 // the loop: split-K over row blocks, each workgroup accumulating the lower
 // 32x32 tiles of its block with v_mfma_f32_32x32x2_f32 (rows staged through
-// LDS by coalesced float4 loads), partial slabs written in block order, then
-// a reduce kernel that sums the slabs in that fixed order (deterministic,
-// no atomics) and mirrors the lower triangle.  Dp = 8, 16 use a VALU path.
+// LDS by coalesced float4 loads), one partial slab per leaf of rows; the
+// leaves of a group are summed in leaf order into the group's slab, and the
+// group slabs in group order into G, mirrored (kernels.h GramPlan: the leaf
+// and group cuts depend only on the row count, so the sum is the same at
+// every world size).  Deterministic, no atomics.  Dp = 8, 16 use a VALU path.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "common.h"
 #include "kernels.h"
@@ -211,63 +215,113 @@ __global__ void __launch_bounds__(256)
   G[j * Dp + i] = s;
 }
 
-template <int T>
-hipError_t launch_tiled(const GramArgs& a, hipStream_t s) {
-  const int64_t rpb = rows_per_block(a.n);
-  const int64_t nblk = (a.n + rpb - 1) / rpb;
-  constexpr int Dp = 32 * T;
-  if (nblk > 0)
-    hipLaunchKernelGGL(gram_tiled_kernel<T>, dim3((unsigned)nblk), dim3(GramCfg<T>::NTHR), 0, s,
-                       a, rpb);
-  else
-    return hipMemsetAsync(a.G, 0, sizeof(float) * Dp * Dp, s);
-  constexpr int NT = T * (T + 1) / 2;
-  hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3(NT * 256 / (256 / kRedChains)), dim3(256), 0, s,
-                     a.partials, nblk, a.G);
-  return hipGetLastError();
+// Sum of a group's leaf partials in leaf order, one thread per float4 of
+// the slab (blockIdx.y = group - g_lo; leaves indexed from the first leaf of
+// group g_lo, as the leaf kernels wrote them).
+__global__ void __launch_bounds__(256)
+    gram_group_kernel(const float4* __restrict__ P, int64_t slab4, int64_t nleaf, int ngroup,
+                      int g_lo, float4* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= slab4) return;
+  const int g = g_lo + (int)blockIdx.y;
+  const int64_t base = (int64_t)g_lo * nleaf / ngroup;
+  const int64_t l0 = (int64_t)g * nleaf / ngroup - base, l1 = (int64_t)(g + 1) * nleaf / ngroup - base;
+  float4 acc = P[l0 * slab4 + q];
+  for (int64_t l = l0 + 1; l < l1; ++l) {
+    const float4 v = P[l * slab4 + q];
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
+  }
+  out[(int64_t)g * slab4 + q] = acc;
 }
 
-template <int Dp>
-hipError_t launch_small(const GramArgs& a, hipStream_t s) {
-  const int64_t rpb = rows_per_block(a.n);
-  const int64_t nblk = (a.n + rpb - 1) / rpb;
-  if (nblk == 0) return hipMemsetAsync(a.G, 0, sizeof(float) * Dp * Dp, s);
-  hipLaunchKernelGGL(gram_small_kernel<Dp>, dim3((unsigned)nblk), dim3(256), 0, s, a, rpb);
-  hipLaunchKernelGGL(gram_small_reduce_kernel<Dp>, dim3(1), dim3(256), 0, s, a.partials, nblk,
-                     a.G);
-  return hipGetLastError();
+template <int T>
+void launch_tiled_leaves(const GramArgs& a, hipStream_t s, int64_t nblk) {
+  hipLaunchKernelGGL(gram_tiled_kernel<T>, dim3((unsigned)nblk), dim3(GramCfg<T>::NTHR), 0, s, a,
+                     a.plan.rpl);
+}
+
+template <int T>
+void launch_tiled_final(const float* gslabs, int64_t ngroup, float* G, hipStream_t s) {
+  constexpr int NT = T * (T + 1) / 2;
+  hipLaunchKernelGGL(gram_reduce_kernel<T>, dim3(NT * 256 / (256 / kRedChains)), dim3(256), 0, s,
+                     gslabs, ngroup, G);
 }
 
 }  // namespace
 
-int64_t gram_num_blocks(int Dp, int64_t n) {
-  (void)Dp;
-  const int64_t rpb = rows_per_block(n);
-  return (n + rpb - 1) / rpb;
-}
-
-size_t gram_workspace_floats(int Dp, int64_t n) {
-  const int64_t nblk = wide_dim(Dp) ? wide_gram_num_blocks(n) : gram_num_blocks(Dp, n);
-  if (Dp <= 16) return (size_t)(nblk > 0 ? nblk : 1) * Dp * Dp;
+GramPlan gram_plan(int Dp, int64_t n) {
+  GramPlan p;
+  p.n = n;
+  p.rpl = wide_dim(Dp) ? wide_rows_per_leaf(n) : rows_per_block(n);
+  p.nleaf = n > 0 ? (n + p.rpl - 1) / p.rpl : 0;
+  p.ngroup = (int)std::min<int64_t>(kGramGroups, p.nleaf);
   const int T = Dp / 32;
-  return (size_t)(nblk > 0 ? nblk : 1) * (T * (T + 1) / 2) * 1024;
+  p.slab_floats = Dp <= 16 ? (size_t)Dp * Dp : (size_t)(T * (T + 1) / 2) * 1024;
+  return p;
 }
 
-hipError_t launch_gramian(int Dp, const GramArgs& a, hipStream_t s) {
-  if (wide_dim(Dp)) return launch_wide_gramian(Dp, a, s);
+size_t gram_leaf_floats(const GramPlan& p, int g_lo, int g_hi) {
+  const int64_t nl = g_hi > g_lo ? gram_group_leaf(p, g_hi) - gram_group_leaf(p, g_lo) : 0;
+  return (size_t)std::max<int64_t>(nl, 1) * p.slab_floats;
+}
+
+hipError_t launch_gramian(int Dp, const GramArgs& in, hipStream_t s) {
+  if (in.g_hi <= in.g_lo) return hipSuccess;
+  GramArgs a = in;
+  const int64_t l0 = gram_group_leaf(a.plan, a.g_lo), l1 = gram_group_leaf(a.plan, a.g_hi);
+  a.row0 = l0 * a.plan.rpl;
+  a.n = std::min(a.plan.n, l1 * a.plan.rpl) - a.row0;
+  const int64_t nblk = l1 - l0;
+  if (wide_dim(Dp)) {
+    hipError_t e = launch_wide_gram_leaves(Dp, a, s);
+    if (e != hipSuccess) return e;
+  } else {
+    switch (Dp) {
+      case 8: hipLaunchKernelGGL(gram_small_kernel<8>, dim3((unsigned)nblk), dim3(256), 0, s, a,
+                                 a.plan.rpl); break;
+      case 16: hipLaunchKernelGGL(gram_small_kernel<16>, dim3((unsigned)nblk), dim3(256), 0, s, a,
+                                  a.plan.rpl); break;
+      case 32: launch_tiled_leaves<1>(a, s, nblk); break;
+      case 64: launch_tiled_leaves<2>(a, s, nblk); break;
+      case 96: launch_tiled_leaves<3>(a, s, nblk); break;
+      case 128: launch_tiled_leaves<4>(a, s, nblk); break;
+      case 160: launch_tiled_leaves<5>(a, s, nblk); break;
+      case 192: launch_tiled_leaves<6>(a, s, nblk); break;
+      case 224: launch_tiled_leaves<7>(a, s, nblk); break;
+      case 256: launch_tiled_leaves<8>(a, s, nblk); break;
+      default: return hipErrorInvalidValue;
+    }
+  }
+  const int64_t slab4 = (int64_t)(a.plan.slab_floats / 4);
+  hipLaunchKernelGGL(gram_group_kernel, dim3((unsigned)((slab4 + 255) / 256), (unsigned)(a.g_hi - a.g_lo)),
+                     dim3(256), 0, s, reinterpret_cast<const float4*>(a.partials), slab4,
+                     a.plan.nleaf, a.plan.ngroup, a.g_lo, reinterpret_cast<float4*>(a.gslabs));
+  return hipGetLastError();
+}
+
+hipError_t launch_gram_final(int Dp, const GramPlan& p, const float* gslabs, float* G,
+                             hipStream_t s) {
+  if (p.ngroup == 0) return hipMemsetAsync(G, 0, sizeof(float) * Dp * Dp, s);
+  if (wide_dim(Dp)) return launch_wide_gram_final(Dp, gslabs, p.ngroup, G, s);
   switch (Dp) {
-    case 8: return launch_small<8>(a, s);
-    case 16: return launch_small<16>(a, s);
-    case 32: return launch_tiled<1>(a, s);
-    case 64: return launch_tiled<2>(a, s);
-    case 96: return launch_tiled<3>(a, s);
-    case 128: return launch_tiled<4>(a, s);
-    case 160: return launch_tiled<5>(a, s);
-    case 192: return launch_tiled<6>(a, s);
-    case 224: return launch_tiled<7>(a, s);
-    case 256: return launch_tiled<8>(a, s);
+    case 8: hipLaunchKernelGGL(gram_small_reduce_kernel<8>, dim3(1), dim3(256), 0, s, gslabs,
+                               (int64_t)p.ngroup, G); break;
+    case 16: hipLaunchKernelGGL(gram_small_reduce_kernel<16>, dim3(1), dim3(256), 0, s, gslabs,
+                                (int64_t)p.ngroup, G); break;
+    case 32: launch_tiled_final<1>(gslabs, p.ngroup, G, s); break;
+    case 64: launch_tiled_final<2>(gslabs, p.ngroup, G, s); break;
+    case 96: launch_tiled_final<3>(gslabs, p.ngroup, G, s); break;
+    case 128: launch_tiled_final<4>(gslabs, p.ngroup, G, s); break;
+    case 160: launch_tiled_final<5>(gslabs, p.ngroup, G, s); break;
+    case 192: launch_tiled_final<6>(gslabs, p.ngroup, G, s); break;
+    case 224: launch_tiled_final<7>(gslabs, p.ngroup, G, s); break;
+    case 256: launch_tiled_final<8>(gslabs, p.ngroup, G, s); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
 }
 
 hipError_t launch_zero_gram(int Dp, float* G, hipStream_t s) {

@@ -55,13 +55,44 @@ struct SolveArgs {
   int64_t n_work;
 };
 
+// Partition-independent Gramian.  The rows of a side are cut
+// into fixed leaves (rows per leaf from the side's row count alone) and the
+// leaves into ngroup = min(kGramGroups, leaves) runs of consecutive leaves.
+// A leaf's partial is one workgroup's fixed-order accumulation, a group's
+// slab the sum of its leaves in leaf order, and G the sum of the group slabs
+// in group order: the same additions whichever rank computes which group, so
+// G is bitwise the same at every world size (ranks own whole groups and
+// exchange group slabs, never partially reduced sums).
+constexpr int kGramGroups = 16;
+struct GramPlan {
+  int64_t n = 0;        // rows of the side
+  int64_t rpl = 0;      // rows per leaf
+  int64_t nleaf = 0;
+  int ngroup = 0;
+  size_t slab_floats = 0;  // floats of one leaf / group slab (lower tiles, or Dp^2 at Dp <= 16)
+};
+GramPlan gram_plan(int Dp, int64_t n);
+inline int64_t gram_group_leaf(const GramPlan& p, int g) {
+  return p.ngroup ? (int64_t)g * p.nleaf / p.ngroup : 0;
+}
+// Groups [lo, hi) of rank `rank` of `world` (contiguous, balanced by count).
+inline void gram_owned_groups(const GramPlan& p, int world, int rank, int* lo, int* hi) {
+  *lo = (int)((int64_t)p.ngroup * rank / world);
+  *hi = (int)((int64_t)p.ngroup * (rank + 1) / world);
+}
+// Leaf-workspace floats for computing groups [g_lo, g_hi).
+size_t gram_leaf_floats(const GramPlan& p, int g_lo, int g_hi);
+
 struct GramArgs {
   const float* X;        // ld = Dp
-  int64_t row0;          // first row
-  int64_t n;             // rows
   const float* w;        // per-row weight (absolute row index) or nullptr
-  float* partials;       // workspace
-  float* G;              // Dp x Dp output (full, symmetric)
+  float* partials;       // leaf workspace (gram_leaf_floats)
+  float* gslabs;         // [plan.ngroup][plan.slab_floats] group slabs
+  GramPlan plan;
+  int g_lo, g_hi;        // groups this launch computes
+  // set by the launcher: rows [row0, row0 + n) = the leaves of the groups
+  int64_t row0;
+  int64_t n;
 };
 
 struct LossArgs {
@@ -79,10 +110,6 @@ struct LossArgs {
   int raw;               // 1: out[e] = sum_j (x_j . u - 1)^2 only (train stats)
 };
 
-// Number of workgroups / partial slabs the Gramian of n rows uses.
-int64_t gram_num_blocks(int Dp, int64_t n);
-// Partial workspace floats needed for n rows at padded dim Dp.
-size_t gram_workspace_floats(int Dp, int64_t n);
 
 // History-space ("dual") solve of the short-history entities (dual.hip).
 // With G = Q T Q^T (Q orthogonal, T tridiagonal) and M = mu*G + lam*I,
@@ -167,7 +194,12 @@ __host__ __device__ inline int64_t blk_v(int64_t p, int k, int Dp) {
 __host__ __device__ inline int64_t blk_t(int64_t p, int j, int k, int Dp) {
   return ((p >> 6) * 3 * Dp + j * Dp + k) * 64 + (p & 63);
 }
+// The leaves of groups [a.g_lo, a.g_hi) into a.partials, each group summed
+// into its slab a.gslabs[g].
 hipError_t launch_gramian(int Dp, const GramArgs& a, hipStream_t s);
+// G = sum of the plan's group slabs in group order, mirrored (Dp x Dp).
+hipError_t launch_gram_final(int Dp, const GramPlan& p, const float* gslabs, float* G,
+                             hipStream_t s);
 
 // iALS++ block step (pp.hip; ialspp.h:85-145, 351-424).
 struct PPArgs {
@@ -214,8 +246,11 @@ size_t wide_slot_floats(int Dp);
 // ([slabs][wide_slab_floats(Dp)]), computed by their own workgroups first.
 int64_t wide_slab_rows();
 size_t wide_slab_floats(int Dp);
-int64_t wide_gram_num_blocks(int64_t n);
-hipError_t launch_wide_gramian(int Dp, const GramArgs& g, hipStream_t s);
+int64_t wide_rows_per_leaf(int64_t n);
+// Leaves of g (rows [g.row0, g.row0 + g.n), leaf size g.plan.rpl) into g.partials.
+hipError_t launch_wide_gram_leaves(int Dp, const GramArgs& g, hipStream_t s);
+hipError_t launch_wide_gram_final(int Dp, const float* gslabs, int64_t ngroup, float* G,
+                                  hipStream_t s);
 hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batch,
                              hipStream_t s);
 size_t wide_tridiag_work_floats(int Dp);
@@ -236,5 +271,9 @@ int padded_dim(int dim);
 // true (default): the SYRK kernels run fp32-accurate split-bf16 MFMA
 // (common.h mfma_x6); FRECSYS_SYRK_F32=1 selects v_mfma_f32_32x32x2_f32.
 bool syrk_split_bf16();
+// true when a gather over `rows` rows of ld Dp needs 64-bit element offsets
+// (rows * Dp >= 2^32), or FRECSYS_GATHER64=1 forces them (tests: the two
+// widths are bit-identical).
+bool gather_off64(int64_t rows, int Dp);
 
 }  // namespace frecsys_hip

@@ -99,7 +99,7 @@ __device__ __forceinline__ int64_t virt_pos(int64_t k, int64_t h) {
 // own workgroup (PARTIAL = false, a.split[pos].y > 0) then starts from the
 // sum of its slabs instead of gathering -- the longest histories (55K rows
 // on the ML-20M item side) no longer serialise on one CU.
-template <int T, bool PARTIAL, bool BF>
+template <int T, bool PARTIAL, bool BF, bool OFF64 = false>
 __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     solve_tiled_kernel(SolveArgs a) {
   using C = TiledCfg<T, BF>;
@@ -214,8 +214,14 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
         // no select on the loaded value: rows past the history have sa = 0
         // (split_bf), so the loads stay in flight through the MFMA phase
 #pragma unroll
-        for (int j = 0; j < 4; ++j)  // 32-bit element offsets (rows x Dp < 2^32, checked at launch)
-          xr[4 * q + j] = a.X[(unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)bc];
+        for (int j = 0; j < 4; ++j) {
+          // 32-bit element offsets while rows x Dp < 2^32 (launch_tiled_v
+          // dispatches OFF64 above that)
+          if constexpr (OFF64)
+            xr[4 * q + j] = a.X[(int64_t)max(id[j], 0) * Dp + bc];
+          else
+            xr[4 * q + j] = a.X[(unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)bc];
+        }
       }
     }
   };
@@ -748,21 +754,32 @@ __global__ void __launch_bounds__(256) solve_small_kernel(SolveArgs a) {
   if (!ok) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
-template <int T, bool PARTIAL, bool BF>
-hipError_t launch_tiled_v(const SolveArgs& a, hipStream_t s) {
+template <int T, bool PARTIAL, bool BF, bool OFF64>
+hipError_t launch_tiled_o(const SolveArgs& a, hipStream_t s) {
   using C = TiledCfg<T, BF>;
   static bool attr = false;
   if (!attr) {
-    hipError_t err = hipFuncSetAttribute((const void*)solve_tiled_kernel<T, PARTIAL, BF>,
+    hipError_t err = hipFuncSetAttribute((const void*)solve_tiled_kernel<T, PARTIAL, BF, OFF64>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)C::BYTES);
     if (err != hipSuccess) return err;
     attr = true;
   }
   const int64_t n = PARTIAL ? a.n_work : a.n_rows;
-  hipLaunchKernelGGL((solve_tiled_kernel<T, PARTIAL, BF>), dim3((unsigned)n), dim3(C::NTHR),
-                     C::BYTES, s, a);
+  hipLaunchKernelGGL((solve_tiled_kernel<T, PARTIAL, BF, OFF64>), dim3((unsigned)n),
+                     dim3(C::NTHR), C::BYTES, s, a);
   return hipGetLastError();
+}
+
+// The split-bf16 gathers use 32-bit element offsets while n_other * Dp <
+// 2^32 (Dp = 256: 16.7M rows), 64-bit ones above (the fp32 staging path
+// always uses 64-bit offsets).
+template <int T, bool PARTIAL, bool BF>
+hipError_t launch_tiled_v(const SolveArgs& a, hipStream_t s) {
+  if constexpr (BF) {
+    if (gather_off64(a.n_other, 32 * T)) return launch_tiled_o<T, PARTIAL, BF, true>(a, s);
+  }
+  return launch_tiled_o<T, PARTIAL, BF, false>(a, s);
 }
 
 template <int T, bool PARTIAL>
@@ -779,6 +796,12 @@ hipError_t launch_small(const SolveArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+bool gather_off64(int64_t rows, int Dp) {
+  if (rows * (int64_t)Dp >= ((int64_t)1 << 32)) return true;
+  const char* v = getenv("FRECSYS_GATHER64");  // tests: force the 64-bit variants
+  return v && atoi(v) != 0;
+}
 
 bool syrk_split_bf16() {
   static const bool on = [] {
@@ -800,7 +823,6 @@ int padded_dim(int dim) {
 
 hipError_t launch_solve(int Dp, const SolveArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;
-  if (a.n_other * (int64_t)Dp >= ((int64_t)1 << 32)) return hipErrorInvalidValue;  // gathers
   switch (Dp) {
     case 8: return launch_small<8>(a, s);
     case 16: return launch_small<16>(a, s);
@@ -818,7 +840,6 @@ hipError_t launch_solve(int Dp, const SolveArgs& a, hipStream_t s) {
 
 hipError_t launch_split_syrk(int Dp, const SolveArgs& a, hipStream_t s) {
   if (a.n_work <= 0) return hipSuccess;
-  if (a.n_other * (int64_t)Dp >= ((int64_t)1 << 32)) return hipErrorInvalidValue;  // gathers
   switch (Dp) {
     case 32: return launch_tiled<1, true>(a, s);
     case 64: return launch_tiled<2, true>(a, s);

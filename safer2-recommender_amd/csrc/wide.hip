@@ -57,7 +57,7 @@ namespace {
 
 constexpr int WB = 128;    // block-pair edge
 constexpr int WR = 16;     // rows per staged chunk
-constexpr int kWideMaxBlocks = 64;
+constexpr int kWideMaxBlocks = 256;  // leaves of a Gramian (kernels.h GramPlan)
 
 __device__ __forceinline__ void pair_of(int pidx, int& BI, int& BJ) {
   BI = 0;
@@ -127,7 +127,7 @@ int wide_pairs2(int Dp) {
   return nb * (nb + 1) / 2;
 }
 
-template <int MODE>
+template <int MODE, bool OFF64 = false>
 __global__ void __launch_bounds__(512)
     wide_syrk2_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws,
                       int64_t n_units) {
@@ -228,9 +228,13 @@ __global__ void __launch_bounds__(512)
       for (int j = 0; j < 4; ++j) {
         // no select on the loaded value (rows past the end have sa = 0): the
         // loads stay in flight through the MFMAs of the current chunk.  32-bit
-        // element offsets (rows x Dp < 2^32, checked at launch)
-        const unsigned off = (unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)xcol;
-        xr[4 * q + j] = FRECSYS_SKIP(a.debug_skip, 32) ? 0.0f : X[off];
+        // element offsets while rows x Dp < 2^32 (OFF64 above: gather_off64)
+        float v;
+        if constexpr (OFF64)
+          v = X[(int64_t)max(id[j], 0) * Dp + xcol];
+        else
+          v = X[(unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)xcol];
+        xr[4 * q + j] = FRECSYS_SKIP(a.debug_skip, 32) ? 0.0f : v;
       }
     }
   };
@@ -1028,23 +1032,26 @@ size_t wide_slab_floats(int Dp) {
   return (size_t)T * (T + 1) / 2 * 1024 + 2 * (size_t)Dp;
 }
 
-int64_t wide_gram_num_blocks(int64_t n) {
-  const int64_t rpb = wide_rows_per_block(n);
-  return (n + rpb - 1) / rpb;
+int64_t wide_rows_per_leaf(int64_t n) { return wide_rows_per_block(n); }
+
+hipError_t launch_wide_gram_leaves(int Dp, const GramArgs& g, hipStream_t s) {
+  if (!wide_dim(Dp)) return hipErrorInvalidValue;
+  const int64_t nblk = (g.n + g.plan.rpl - 1) / g.plan.rpl;
+  if (nblk <= 0) return hipSuccess;
+  SolveArgs a{};
+  if (gather_off64(g.row0 + g.n, Dp))
+    hipLaunchKernelGGL((wide_syrk2_kernel<0, true>), dim3(xcd_grid(nblk, wide_pairs2(Dp))),
+                       dim3(512), 0, s, a, g, Dp, g.plan.rpl, (int64_t)0, (float*)nullptr, nblk);
+  else
+    hipLaunchKernelGGL((wide_syrk2_kernel<0, false>), dim3(xcd_grid(nblk, wide_pairs2(Dp))),
+                       dim3(512), 0, s, a, g, Dp, g.plan.rpl, (int64_t)0, (float*)nullptr, nblk);
+  return hipGetLastError();
 }
 
-hipError_t launch_wide_gramian(int Dp, const GramArgs& g, hipStream_t s) {
-  if (!wide_dim(Dp)) return hipErrorInvalidValue;
-  // 32-bit element offsets in the row gathers
-  if ((g.row0 + g.n) * (int64_t)Dp >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
-  const int64_t rpb = wide_rows_per_block(g.n);
-  const int64_t nblk = (g.n + rpb - 1) / rpb;
-  if (nblk == 0) return hipMemsetAsync(g.G, 0, sizeof(float) * Dp * Dp, s);
-  SolveArgs a{};
-  hipLaunchKernelGGL(wide_syrk2_kernel<0>, dim3(xcd_grid(nblk, wide_pairs2(Dp))), dim3(512), 0, s,
-                     a, g, Dp, rpb, (int64_t)0, (float*)nullptr, nblk);
+hipError_t launch_wide_gram_final(int Dp, const float* gslabs, int64_t ngroup, float* G,
+                                  hipStream_t s) {
   hipLaunchKernelGGL(wide_gram_reduce_kernel, dim3((unsigned)(((int64_t)Dp * Dp + 255) / 256)),
-                     dim3(256), 0, s, g.partials, nblk, g.G, Dp);
+                     dim3(256), 0, s, gslabs, ngroup, G, Dp);
   return hipGetLastError();
 }
 
@@ -1052,8 +1059,7 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                              hipStream_t s) {
   if (!wide_dim(Dp) || batch <= 0) return hipErrorInvalidValue;
   if (a.n_rows <= 0) return hipSuccess;
-  // 32-bit element offsets in the row gathers
-  if (a.n_other * (int64_t)Dp >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+  const bool off64 = gather_off64(a.n_other, Dp);
   static bool attr = false;
   if (!attr) {
     hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel<16>,
@@ -1071,13 +1077,21 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
   // the slabs of the long histories (all in the first batch) first
   if (a.n_work > 0) {
     if (a.n_split > std::min<int64_t>(batch, a.n_rows)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(wide_syrk2_kernel<2>, dim3(xcd_grid(a.n_work, wide_pairs2(Dp))), dim3(512),
-                       0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
+    if (off64)
+      hipLaunchKernelGGL((wide_syrk2_kernel<2, true>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
+    else
+      hipLaunchKernelGGL((wide_syrk2_kernel<2, false>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
   }
   for (int64_t s0 = 0; s0 < a.n_rows; s0 += batch) {
     const int64_t nb = std::min<int64_t>(batch, a.n_rows - s0);
-    hipLaunchKernelGGL(wide_syrk2_kernel<1>, dim3(xcd_grid(nb, wide_pairs2(Dp))), dim3(512), 0, s,
-                       a, g, Dp, (int64_t)0, s0, ws, nb);
+    if (off64)
+      hipLaunchKernelGGL((wide_syrk2_kernel<1, true>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
+    else
+      hipLaunchKernelGGL((wide_syrk2_kernel<1, false>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
     else if (Dp == 512)

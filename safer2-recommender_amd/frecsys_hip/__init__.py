@@ -37,14 +37,16 @@ EXPORTS = (
     "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset", "frecsys_debug_basis",
     "frecsys_eval_topk", "frecsys_train_stats", "frecsys_pp_set_rating_index",
     "frecsys_pp_predict", "frecsys_pp_step", "frecsys_debug_diag_factor",
-    "frecsys_history_space_max_h",
+    "frecsys_history_space_max_h", "frecsys_comm_world", "frecsys_gram_groups",
+    "frecsys_get_gram_groups", "frecsys_set_gram_groups", "frecsys_get_gramian",
+    "frecsys_gram_plan",
 )
 
 # Every symbol include/frecsys_model.h declares.
 MODEL_EXPORTS = (
     "frecsys_model_config_default", "frecsys_model_create", "frecsys_model_initialize",
     "frecsys_model_train", "frecsys_model_context", "frecsys_model_mean_weight",
-    "frecsys_model_destroy", "frecsys_model_last_error",
+    "frecsys_model_destroy", "frecsys_model_last_error", "frecsys_model_dual_state",
 )
 
 
@@ -122,6 +124,12 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, P]),
         "frecsys_timing_reset": (ctypes.c_int, [P]),
         "frecsys_history_space_max_h": (I32, [P]),
+        "frecsys_comm_world": (ctypes.c_int, [P, P, P, P]),
+        "frecsys_gram_groups": (ctypes.c_int, [P, I32, P, P, P, P]),
+        "frecsys_get_gram_groups": (ctypes.c_int, [P, I32, P]),
+        "frecsys_set_gram_groups": (ctypes.c_int, [P, I32, P]),
+        "frecsys_get_gramian": (ctypes.c_int, [P, I32, P, I64]),
+        "frecsys_gram_plan": (ctypes.c_int, [I32, I64, I32, I32, P, P, P, P, P]),
         "frecsys_debug_basis": (ctypes.c_int, [P, I32, P, P, P]),
         "frecsys_debug_diag_factor": (ctypes.c_int, [P, I32, I32, P, P, P]),
         "frecsys_eval_topk": (ctypes.c_int, [P, I32, P]),
@@ -157,6 +165,7 @@ def load_model_library(path: str = MODEL_LIB_PATH) -> ctypes.CDLL:
         "frecsys_model_mean_weight": (ctypes.c_float, [P]),
         "frecsys_model_destroy": (None, [P]),
         "frecsys_model_last_error": (ctypes.c_char_p, []),
+        "frecsys_model_dual_state": (ctypes.c_int, [P, P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -190,6 +199,19 @@ def partition(row_ptr: np.ndarray, nparts: int) -> np.ndarray:
     if rc:
         raise FrecsysError(rc, lib.frecsys_last_error(None).decode())
     return out
+
+
+def gram_plan(dim: int, n_rows: int, world: int = 1, rank: int = 0):
+    """Host-only Gramian plan: (rows_per_leaf, n_leaves, n_groups, own_lo,
+    own_hi) -- frecsys_gram_plan."""
+    lib = load_library()
+    rpl, nl = ctypes.c_int64(), ctypes.c_int64()
+    ng, lo, hi = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+    rc = lib.frecsys_gram_plan(dim, n_rows, world, rank, ctypes.byref(rpl), ctypes.byref(nl),
+                               ctypes.byref(ng), ctypes.byref(lo), ctypes.byref(hi))
+    if rc:
+        raise FrecsysError(rc, lib.frecsys_last_error(None).decode())
+    return int(rpl.value), int(nl.value), int(ng.value), int(lo.value), int(hi.value)
 
 
 def unique_id() -> bytes:
@@ -253,6 +275,32 @@ class Context:
         buf = None if uid is None else (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         self._check(self.lib.frecsys_comm_init(self.h, world, rank, buf))
 
+    def comm_world(self) -> Tuple[int, int, int]:
+        """(world, rank, ranks of the RCCL communicator -- 0 without one)."""
+        w, r, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.lib.frecsys_comm_world(self.h, ctypes.byref(w), ctypes.byref(r),
+                                                ctypes.byref(n)))
+        return int(w.value), int(r.value), int(n.value)
+
+    def gram_groups(self, side: int) -> Tuple[int, int, int, int]:
+        """(n_groups, own_lo, own_hi, floats_per_group) of side's Gramian plan."""
+        ng, lo, hi, fl = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        self._check(self.lib.frecsys_gram_groups(self.h, side, ctypes.byref(ng), ctypes.byref(lo),
+                                                 ctypes.byref(hi), ctypes.byref(fl)))
+        return int(ng.value), int(lo.value), int(hi.value), int(fl.value)
+
+    def get_gram_groups(self, side: int) -> np.ndarray:
+        ng, _, _, fl = self.gram_groups(side)
+        out = np.zeros((ng, fl), dtype=np.float32)
+        self._check(self.lib.frecsys_get_gram_groups(self.h, side, _ptr(out)))
+        return out
+
+    def set_gram_groups(self, side: int, slabs: np.ndarray):
+        ng, _, _, fl = self.gram_groups(side)
+        a = np.ascontiguousarray(slabs, dtype=np.float32)
+        assert a.shape == (ng, fl), (a.shape, ng, fl)
+        self._check(self.lib.frecsys_set_gram_groups(self.h, side, _ptr(a)))
+
     def shard_range(self, side: int) -> Tuple[int, int]:
         lo, hi = ctypes.c_int64(), ctypes.c_int64()
         self._check(self.lib.frecsys_shard_range(self.h, side, ctypes.byref(lo), ctypes.byref(hi)))
@@ -289,6 +337,12 @@ class Context:
         out = np.empty((self.dim, self.dim), dtype=np.float32) if fetch else None
         self._check(self.lib.frecsys_gramian(self.h, side, _ptr(w), 1 if from_snapshot else 0,
                                              _ptr(out)))
+        return out
+
+    def get_gramian(self, side: int) -> np.ndarray:
+        """G[side] as the context holds it (no recomputation)."""
+        out = np.empty((self.dim, self.dim), dtype=np.float32)
+        self._check(self.lib.frecsys_get_gramian(self.h, side, _ptr(out), self.dim))
         return out
 
     def set_gramian(self, side: int, G: np.ndarray):
@@ -434,8 +488,22 @@ class Model:
 
     def context(self) -> Context:
         """The model's device context (borrowed: closing it is a no-op)."""
-        return Context(self.dim, self.n_users, self.n_items,
-                       _borrowed=self.lib.frecsys_model_context(self.h))
+        ctx = Context(self.dim, self.n_users, self.n_items,
+                      _borrowed=self.lib.frecsys_model_context(self.h))
+        ctx._owner = self  # the native context lives as long as the model
+        return ctx
+
+    def dual_state(self):
+        """(omega [n_users], user losses [n_users], item_reg [n_items], xi) of
+        ERM-MF / CVaR-MF / SAFER2 (frecsys_model_dual_state)."""
+        w = np.zeros(self.n_users, dtype=np.float32)
+        l = np.zeros(self.n_users, dtype=np.float32)
+        r = np.zeros(self.n_items, dtype=np.float32)
+        xi = ctypes.c_float(0.0)
+        rc = self.lib.frecsys_model_dual_state(self.h, _ptr(w), _ptr(l), _ptr(r), ctypes.byref(xi))
+        if rc:
+            raise FrecsysError(rc, self.lib.frecsys_model_last_error().decode())
+        return w, l, r, float(xi.value)
 
     def mean_weight(self) -> float:
         return float(self.lib.frecsys_model_mean_weight(self.h))

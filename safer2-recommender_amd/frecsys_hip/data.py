@@ -15,13 +15,28 @@ BASELINE.md section 4 directly in CSR (no CSV).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
 
 
+def _stable_order(rows: np.ndarray) -> np.ndarray:
+    """np.argsort(rows, kind="stable") for non-negative ints: when row and
+    position fit one int64 the (row, position) keys are distinct, so an
+    unstable sort of them gives the same order, several times faster."""
+    n = len(rows)
+    pbits = max(int(n - 1).bit_length(), 1)
+    if n == 0 or int(rows.max()).bit_length() + pbits > 63:
+        return np.argsort(rows, kind="stable")
+    key = (rows.astype(np.int64) << pbits) | np.arange(n, dtype=np.int64)
+    key.sort()
+    key &= (1 << pbits) - 1
+    return key
+
+
 def _csr_from_pairs(rows: np.ndarray, cols: np.ndarray, n_rows: int):
-    order = np.argsort(rows, kind="stable")  # keeps file order inside a row
+    order = _stable_order(rows)  # keeps file order inside a row
     counts = np.bincount(rows, minlength=n_rows)
     row_ptr = np.zeros(n_rows + 1, dtype=np.int64)
     np.cumsum(counts, out=row_ptr[1:])
@@ -83,6 +98,58 @@ SHAPES = {
 }
 
 
+def _searchsorted_uniform(cdf: np.ndarray, r: np.ndarray, log2_buckets: int = 24) -> np.ndarray:
+    """np.searchsorted(cdf, r) (side 'left') for r in [0, 1), bucketed: with
+    M = 2^k buckets the edges j/M are exact doubles and r*M floors exactly, so
+    the answer for r in bucket j lies in [S[j], S[j+1]], S = searchsorted of
+    the edges.  Buckets with S[j] == S[j+1] are answered by the table; the
+    rest fall back to searchsorted.  Identical output, without the random
+    accesses of one binary search per sample (2M x 500K: 74 s -> a few)."""
+    M = 1 << log2_buckets
+    S = np.searchsorted(cdf, np.arange(M + 1, dtype=np.float64) / M).astype(np.int64)
+    j = (r * M).astype(np.int64)
+    lo = S[j]
+    amb = np.nonzero(S[j + 1] != lo)[0]
+    if len(amb):
+        lo[amb] = np.searchsorted(cdf, r[amb])
+    return lo
+
+
+def _first_per_user(users: np.ndarray, items: np.ndarray, nu: int) -> np.ndarray:
+    """Positions of the first occurrence of each (user, item) pair, ascending
+    -- np.unique(users * n_items + items, return_index=True)[1] sorted, for
+    users in non-decreasing order: pairs never repeat across users, so the
+    array is cut at user boundaries and the cuts are deduplicated on threads."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = len(users)
+    nch = max(1, min(16, n // 4_000_000))
+    cuts = [0] + [int(np.searchsorted(users, users[min(n - 1, n * k // nch)], "left"))
+                  for k in range(1, nch)] + [n]
+    cuts = sorted(set(cuts))
+
+    def one(k):
+        a, b = cuts[k], cuts[k + 1]
+        # (item, position) keys within the cut: item-major, position-minor
+        u0 = users[a:b] - users[a]
+        pbits = max(int(b - a - 1).bit_length(), 1)
+        ibits = max(int(items[a:b].max()).bit_length(), 1)
+        if int(u0[-1]).bit_length() + ibits + pbits <= 63:
+            key = (((u0 << ibits) | items[a:b]) << pbits) | np.arange(b - a, dtype=np.int64)
+            key.sort()
+            pk = key >> pbits
+            keep = np.ones(len(key), dtype=bool)
+            keep[1:] = pk[1:] != pk[:-1]
+            pos = key[keep] & ((1 << pbits) - 1)
+        else:
+            _, pos = np.unique(u0 * (1 << ibits) + items[a:b], return_index=True)
+        pos.sort()
+        return pos + a
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+        parts = list(ex.map(one, range(len(cuts) - 1)))
+    return np.concatenate(parts) if parts else np.zeros(0, np.int64)
+
+
 def synthetic(shape: SynthShape, seed: int = 98765):
     """Deterministic synthetic interactions: Zipf-Mandelbrot
     item popularity 1/(rank+q)^s (s=1, q=10: the most popular item reaches
@@ -105,11 +172,9 @@ def synthetic(shape: SynthShape, seed: int = 98765):
     draw = (lens * 1.6 + 8).astype(np.int64)
     tot = int(draw.sum())
     users = np.repeat(np.arange(nu, dtype=np.int64), draw)
-    items = np.searchsorted(cdf, rng.random(tot)).astype(np.int64)
+    items = _searchsorted_uniform(cdf, rng.random(tot))
     np.minimum(items, ni - 1, out=items)
-    key = users * ni + items
-    _, first = np.unique(key, return_index=True)
-    first.sort()
+    first = _first_per_user(users, items, nu)
     users, items = users[first], items[first]
     # rank inside the user (positions kept in draw order), keep < lens[u]
     starts = np.zeros(nu + 1, dtype=np.int64)

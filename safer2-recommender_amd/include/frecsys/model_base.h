@@ -49,6 +49,10 @@ class DeviceModel : public Recommender {
     OnEmbeddingsSet();
   }
   const VectorXf& user_loss() const { return user_loss_; }
+  // The dual state of ERM-MF / CVaR-MF / SAFER2 (empty for iALS): omega as
+  // the last Train() used it, and item_reg_ from Initialize().
+  const VectorXf& dual_weights() const { return dual_weight_; }
+  const VectorXf& item_regularization() const { return item_reg_; }
   DeviceContext& device() { return *dev_; }
 
  protected:

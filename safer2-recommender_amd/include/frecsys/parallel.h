@@ -41,12 +41,16 @@ class ThreadPool {
   int size() const { return (int)workers_.size() + 1; }
 
   // fn(lo, hi) over [0, n) in contiguous ranges; the caller runs one range.
-  // Small n runs inline.
+  // Small n runs inline, and so does a call made while the pool serves
+  // another caller (models trained from two host threads, or a nested call):
+  // the pool holds one job at a time, and the per-index results do not
+  // depend on the split.
   void ParallelFor(int64_t n, int64_t min_per_task,
                    const std::function<void(int64_t, int64_t)>& fn) {
     const int64_t tasks =
         std::max<int64_t>(1, std::min<int64_t>(size(), n / std::max<int64_t>(1, min_per_task)));
-    if (tasks <= 1 || workers_.empty()) {
+    std::unique_lock<std::mutex> owner(call_mu_, std::try_to_lock);
+    if (tasks <= 1 || workers_.empty() || !owner.owns_lock()) {
       if (n > 0) fn(0, n);
       return;
     }
@@ -101,6 +105,7 @@ class ThreadPool {
   }
 
   std::vector<std::thread> workers_;
+  std::mutex call_mu_;  // held by the caller whose job the pool runs
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(int64_t, int64_t)>* job_ = nullptr;

@@ -137,6 +137,30 @@ float frecsys_model_mean_weight(const frecsys_model* m) {
   return NAN;
 }
 
+int frecsys_model_dual_state(const frecsys_model* m, float* weights, float* losses,
+                             float* item_reg, float* xi) {
+  if (!m) return model_fail(FRECSYS_ERR_INVALID, "null model");
+  const frecsys::detail::DeviceModel* dm = frecsys::AsDeviceModel(m->rec.get());
+  const frecsys::VectorXf& w = dm->dual_weights();
+  if ((weights || item_reg) && w.size() == 0)
+    return model_fail(FRECSYS_ERR_INVALID, m->name + " has no dual weights");
+  if (weights) std::memcpy(weights, w.data(), sizeof(float) * (size_t)w.size());
+  if (losses) {
+    const frecsys::VectorXf& l = dm->user_loss();
+    std::memcpy(losses, l.data(), sizeof(float) * (size_t)l.size());
+  }
+  if (item_reg) {
+    const frecsys::VectorXf& r = dm->item_regularization();
+    std::memcpy(item_reg, r.data(), sizeof(float) * (size_t)r.size());
+  }
+  if (xi) {
+    *xi = NAN;
+    if (m->name == "safer2" || m->name == "safer2pp")
+      *xi = static_cast<const frecsys::SAFER2Recommender*>(m->rec.get())->xi();
+  }
+  return FRECSYS_OK;
+}
+
 void frecsys_model_destroy(frecsys_model* m) { delete m; }
 
 const char* frecsys_model_last_error(void) { return g_model_error.c_str(); }

@@ -1,9 +1,9 @@
 """The RCCL exchange code of the sharded path, executed on one GPU: a
 world-1 communicator (frecsys_comm_init with a unique id) makes every
-collective of a half-step run -- ncclAllReduce of the Gramian, the grouped
-ncclBroadcast all-gather of factor rows and of the user losses, and the
-ncclMin agreement on a failed pivot (include/frecsys_hip.h, capi.hip).
-Results must be bit-identical to the communicator-free context.
+collective of a half-step run -- the grouped ncclBroadcast all-gather of the
+Gramian's group slabs, the all-gather of factor rows and of the user losses,
+and the ncclMin agreement on a failed pivot (include/frecsys_hip.h,
+capi.hip).  Results must be bit-identical to the communicator-free context.
 """
 import numpy as np
 import pytest
@@ -42,10 +42,12 @@ def test_world1_rccl_matches_no_comm(quirk_data, dim):
     ctx, _, _ = _ctx(dim, nu, ni, up, uc, ip, ic)
     ctx.comm_init(1, 0, fh.unique_id())
     got = _epoch(ctx, nu, ni, up, ip, ic)
-    # every collective site ran through RCCL (the closing plain Gramian of the
-    # item side repeats the one before the loss on unchanged rows: reused,
-    # no all-reduce -- every rank makes the same reuse decision)
-    assert ctx.timing("allreduce")[1] >= 4
+    # every collective site ran through RCCL: the four Gramians formed, and
+    # not the closing plain Gramian of the item side, which repeats the one
+    # before the loss on unchanged rows -- reused, no exchange (every rank
+    # makes the same reuse decision, so the collectives stay matched)
+    assert ctx.comm_world() == (1, 0, 1)
+    assert ctx.timing("gram_exchange")[1] == 4
     assert ctx.timing("allgather")[1] >= 4
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)

@@ -26,7 +26,7 @@ def _epoch(ctx, reg=0.003, w=0.1):
     return ctx.user_loss(fh.SIDE_USER, w, False)
 
 
-@pytest.mark.parametrize("dim", [64, 128, 256])
+@pytest.mark.parametrize("dim", [64, 128, 256, 512, 1000])
 def test_eager_epochs_bitwise(quirk_data, monkeypatch, dim):
     nu, ni, up, uc, ip, ic = quirk_data
     out = []

@@ -111,8 +111,9 @@ def test_weighted_u(quirk_data, dim):
 
 def _v_inputs(nu, ni, up, ip, ic, om):
     h = np.diff(up).astype(np.float32)
-    with np.errstate(divide="ignore"):
-        nu_w = (om / h).astype(np.float32)
+    # nu_u = omega_u / |H_u| (safer2.h:499-501); an idle user (h = 0) is in no
+    # item's history, so its nu is never read: pass 0 instead of inf / NaN
+    nu_w = np.where(h > 0, om / np.maximum(h, 1), 0).astype(np.float32)
     item_reg = np.zeros(ni, np.float32)
     for v in range(ni):
         acc = np.float32(0)

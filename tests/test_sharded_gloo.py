@@ -1,13 +1,17 @@
-"""world_size-2 rehearsal of the sharded half-step on CPU (gloo).
+"""world_size-2 rehearsal of the sharded half-step's host protocol on CPU
+(gloo; no GPU here -- tests/test_sharded_gloo_gpu.py runs the same exchange
+between processes driving the real HIP kernels on the GPU box).
 
-The product's N>1 path (capi.hip) is: partial Gramian over the rank's own
-rows -> all-reduce; solve the rank's nnz-balanced row range
-(frecsys_partition, called here through the real C-ABI) -> all-gather of the
-updated rows.  Here each gloo rank runs its shard with the CPU oracle as the
-stand-in solver and the collectives through torch.distributed; the test
-checks that the sharded half-step reproduces the single-process one
-(bit-exact solves: they are per-entity independent; Gramian within fp32
-summation order).
+The product's N>1 path (capi.hip) is: the rank's groups of the partition-
+independent Gramian plan (frecsys_gram_plan, called here through the real
+C-ABI: fixed leaves of rows, fixed groups of leaves, each rank a contiguous
+run of groups) -> all-gather of the group slabs -> every rank sums the slabs
+in group order; solve the rank's nnz-balanced row range (frecsys_partition,
+real C-ABI) -> all-gather of the updated rows.  Each gloo rank computes its
+leaves and solves its rows with the CPU oracle (the arithmetic stand-in for
+the kernels), the collectives go through torch.distributed, and the result
+must equal the single-process one BIT FOR BIT: the solves are per-entity
+independent and the Gramian's additions do not depend on the rank count.
 """
 import os
 import socket
@@ -30,6 +34,29 @@ def _free_port():
     return p
 
 
+def group_slabs(X, d, world, rank):
+    """This rank's group slabs of the plan (zeros elsewhere): each leaf's
+    partial Gramian, summed in leaf order within the group (float32)."""
+    rpl, nleaf, ng, lo, hi = fh.gram_plan(d, X.shape[0], world, rank)
+    slabs = np.zeros((ng, d, d), np.float32)
+    for g in range(lo, hi):
+        for leaf in range(g * nleaf // ng, (g + 1) * nleaf // ng):
+            slabs[g] += O_gramian(X[leaf * rpl:(leaf + 1) * rpl])
+    return slabs
+
+
+def O_gramian(X):
+    import oracle as O
+    return O.gramian(X, nthreads=1).astype(np.float32)
+
+
+def finish_gramian(slabs):
+    G = np.zeros(slabs.shape[1:], np.float32)
+    for s in slabs:  # group order
+        G += s
+    return G
+
+
 def _worker(rank, world, port, q):
     import oracle as O
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -38,11 +65,11 @@ def _worker(rank, world, port, q):
     nu, ni, up, uc, ip, ic = make_quirk_data(seed=13, n_users=300, n_items=200)
     d = 12
     U, V = O.init_embeddings(7, 0.1, d, nu, ni)
-    # item Gramian: partial over this rank's item rows, all-reduced
-    bi = fh.partition(ip, world)
-    Gp = torch.from_numpy(O.gramian(V[bi[rank]:bi[rank + 1]], nthreads=1).astype(np.float64))
-    dist.all_reduce(Gp)
-    G = Gp.numpy().astype(np.float32)
+    # item Gramian: this rank's groups, the slabs all-gathered (a sum over
+    # zero-filled arrays: one non-zero contributor per element, exact)
+    sl = torch.from_numpy(group_slabs(V, d, world, rank))
+    dist.all_reduce(sl)
+    G = finish_gramian(sl.numpy())
     # user half-step on this rank's nnz-balanced range
     bu = fh.partition(up, world)
     lo, hi = int(bu[rank]), int(bu[rank + 1])
@@ -78,7 +105,19 @@ def test_sharded_user_halfstep_matches_single(world):
         assert p.exitcode == 0
     nu, ni, up, uc, ip, ic = make_quirk_data(seed=13, n_users=300, n_items=200)
     U, V = O.init_embeddings(7, 0.1, 12, nu, ni)
-    Gs = O.gramian(V, nthreads=1)
-    np.testing.assert_allclose(G, Gs, rtol=1e-5, atol=1e-6)
-    Ur, _ = O.step(up, uc, V, G, 0, 0.003, 0.1, out=U.copy(), nthreads=1)
+    G1 = finish_gramian(group_slabs(V, 12, 1, 0))  # the single-process plan
+    np.testing.assert_array_equal(G, G1)
+    np.testing.assert_allclose(G, O.gramian(V, nthreads=1), rtol=1e-5, atol=1e-6)
+    Ur, _ = O.step(up, uc, V, G1, 0, 0.003, 0.1, out=U.copy(), nthreads=1)
     np.testing.assert_array_equal(Ug, Ur)
+
+
+def test_gram_plan_tiles_groups():
+    """Host-only plan: the ranks' groups tile [0, n_groups) for any world."""
+    for d, n in ((12, 200), (256, 116_677), (512, 471_355), (1024, 2_000_000), (64, 5)):
+        rpl, nleaf, ng, _, _ = fh.gram_plan(d, n)
+        assert (nleaf - 1) * rpl < n <= nleaf * rpl and 1 <= ng <= 16
+        for world in (1, 2, 3, 8, 16, 24):
+            own = [fh.gram_plan(d, n, world, r)[3:] for r in range(world)]
+            assert own[0][0] == 0 and own[-1][1] == ng
+            assert all(a[1] == b[0] and a[0] <= a[1] for a, b in zip(own, own[1:]))

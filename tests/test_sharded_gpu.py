@@ -7,17 +7,17 @@ id): each context computes the partial Gramian over its own rows, solves
 only its nnz-balanced row range (its own LPT queue, its own d-space /
 history-space split) and computes the loss of its own users -- exactly what
 a rank does between collectives -- while the test performs the exchange the
-library does over RCCL (sum of partial Gramians = ncclAllReduce; rows of
-every rank copied to all = the grouped ncclBroadcast all-gather; losses
-likewise).  The result must match the single-context run: solves are
-per-entity independent, so the only difference is the Gramian's summation
-order (fp32 noise, well inside the 1e-4 bar).
+library does over RCCL (the Gramian's group slabs gathered from their owners
+= the grouped ncclBroadcast of frecsys_gramian, then summed in group order by
+frecsys_set_gram_groups; rows of every rank copied to all = the factor
+all-gather; losses likewise).  The result must equal the single-context run
+BIT FOR BIT: solves are per-entity independent and the Gramian
+is partition-independent (fixed leaves and groups, fixed summation order).
 """
 import numpy as np
 import pytest
 
 import frecsys_hip as fh
-from conftest import rel_rows
 
 pytestmark = pytest.mark.gpu
 
@@ -39,10 +39,21 @@ def _allreduce_gram(ctxs, side, weights=None):
     parts = [c.gramian(side, weights) for c in ctxs]
     if len(ctxs) == 1:
         return parts[0]
-    G = np.sum(np.stack(parts).astype(np.float64), axis=0).astype(np.float32)
+    # the exchange frecsys_gramian does over RCCL: every group slab from its owner
+    slabs = None
     for c in ctxs:
-        c.set_gramian(side, G)
-    return G
+        ng, lo, hi, _ = c.gram_groups(side)
+        mine = c.get_gram_groups(side)
+        if slabs is None:
+            slabs = np.zeros_like(mine)
+        assert not mine[:lo].any() and not mine[hi:].any()  # only its own groups
+        slabs[lo:hi] = mine[lo:hi]
+    owned = sorted(c.gram_groups(side)[1:3] for c in ctxs)
+    assert owned[0][0] == 0 and owned[-1][1] == slabs.shape[0]
+    assert all(a[1] == b[0] for a, b in zip(owned, owned[1:]))  # the ranks tile the groups
+    for c in ctxs:
+        c.set_gram_groups(side, slabs)
+    return ctxs[0].get_gramian(side)
 
 
 def _allgather_rows(ctxs, side):
@@ -93,7 +104,7 @@ def ml1m_csr(ml1m):
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
-@pytest.mark.parametrize("dim", [32, 64, 256])
+@pytest.mark.parametrize("dim", [8, 32, 64, 256, 512])
 def test_sharded_ials_matches_single(ml1m_csr, world, dim):
     nu, ni, up, uc, ip, ic = ml1m_csr
     reg, w = 0.003, 0.1
@@ -108,61 +119,30 @@ def test_sharded_ials_matches_single(ml1m_csr, world, dim):
                                                          for r in range(world)]
     Uw, Vw = _ials_epochs(ctxs, 2, reg, w)
     _close(ctxs)
-    eu, ev = rel_rows(Uw, U1), rel_rows(Vw, V1)
-    assert eu.max() < 1e-4 and ev.max() < 1e-4, (eu.max(), ev.max())
+    np.testing.assert_array_equal(Uw, U1)
+    np.testing.assert_array_equal(Vw, V1)
 
 
-def test_sharded_rank_touches_only_its_rows(ml1m_csr):
-    """Without the exchange, a rank's solve leaves every other row as it was."""
+@pytest.mark.parametrize("dim", [8, 64, 256, 512])
+def test_gramian_partition_independent(ml1m_csr, dim):
+    """G (plain and omega-weighted) is bitwise the same for world 1, 2, 3, 8,
+    and on every rank."""
     nu, ni, up, uc, ip, ic = ml1m_csr
-    ctxs = _contexts(3, 64, nu, ni, up, uc, ip, ic)
-    U0 = ctxs[1].get_embeddings(fh.SIDE_USER)
-    _allreduce_gram(ctxs, fh.SIDE_ITEM)
-    ctxs[1].solve_side(fh.SIDE_USER, fh.KIND_IALS, 0.003, 0.1)
-    U = ctxs[1].get_embeddings(fh.SIDE_USER)
-    lo, hi = ctxs[1].shard_range(fh.SIDE_USER)
-    assert 0 < lo < hi < nu
-    assert np.array_equal(U[:lo], U0[:lo]) and np.array_equal(U[hi:], U0[hi:])
-    assert not np.array_equal(U[lo:hi], U0[lo:hi])
-    _close(ctxs)
-
-
-@pytest.mark.parametrize("world", [2, 8])
-def test_sharded_safer2_halfsteps_match_single(ml1m_csr, world):
-    """SAFER2's weighted kinds and the gathered loss on shards
-    (safer2.h:277-299): ProjectU with omega, the omega-weighted U Gramian,
-    ProjectV with nu and the item regulariser (tail quirk on), V^T V, loss."""
-    nu, ni, up, uc, ip, ic = ml1m_csr
-    dim, reg, w, alpha = 64, 0.004, 0.004, 0.3
-    rng = np.random.default_rng(5)
-    omega = rng.uniform(0.05, 1.0, nu).astype(np.float32)
-    hu = np.diff(up).astype(np.float32)
-    nu_w = np.where(hu > 0, omega / np.maximum(hu, 1), 0).astype(np.float32)
-    item_reg = np.zeros(ni, np.float32)
-    inv_h = np.where(hu > 0, 1.0 / np.maximum(hu, 1), 0).astype(np.float32)
-    for i in range(ni):
-        for u in ic[ip[i]:ip[i + 1]]:
-            item_reg[i] += inv_h[u]
-
-    def run(world_):
-        ctxs = _contexts(world_, dim, nu, ni, up, uc, ip, ic)
-        _allreduce_gram(ctxs, fh.SIDE_ITEM)
-        for c in ctxs:
-            c.solve_side(fh.SIDE_USER, fh.KIND_WEIGHTED_U, reg, w, alpha=alpha, entity_weight=omega)
-        _allgather_rows(ctxs, fh.SIDE_USER)
-        _allreduce_gram(ctxs, fh.SIDE_USER, weights=omega)
-        for c in ctxs:
-            c.solve_side(fh.SIDE_ITEM, fh.KIND_WEIGHTED_V, reg, w, alpha=alpha,
-                         entity_reg=item_reg, other_weight=nu_w)
-        _allgather_rows(ctxs, fh.SIDE_ITEM)
-        _allreduce_gram(ctxs, fh.SIDE_ITEM)
-        loss = _allgather_loss(ctxs, w)
-        U, V = ctxs[0].get_embeddings(fh.SIDE_USER), ctxs[0].get_embeddings(fh.SIDE_ITEM)
+    omega = np.random.default_rng(3).uniform(0.05, 1.0, nu).astype(np.float32)
+    cases = ((fh.SIDE_USER, None), (fh.SIDE_ITEM, None), (fh.SIDE_USER, omega))
+    ref = None
+    for world in (1, 2, 3, 8):
+        ctxs = _contexts(world, dim, nu, ni, up, uc, ip, ic)
+        Gs = []
+        for side, wts in cases:
+            _allreduce_gram(ctxs, side, wts)
+            Gs.append([c.get_gramian(side) for c in ctxs])
         _close(ctxs)
-        return U, V, loss
-
-    U1, V1, l1 = run(1)
-    Uw, Vw, lw = run(world)
-    eu, ev = rel_rows(Uw, U1), rel_rows(Vw, V1)
-    assert eu.max() < 1e-4 and ev.max() < 1e-4, (eu.max(), ev.max())
-    np.testing.assert_allclose(lw, l1, rtol=1e-4, atol=1e-7)
+        for G in Gs:
+            for g in G[1:]:
+                np.testing.assert_array_equal(g, G[0])
+        if ref is None:
+            ref = [G[0] for G in Gs]
+        else:
+            for G, R in zip(Gs, ref):
+                np.testing.assert_array_equal(G[0], R)

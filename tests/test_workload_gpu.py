@@ -98,10 +98,13 @@ def test_ials_ml20m_d256_half_steps(ml20m):
     ctx.close()
 
 
-def test_safer2_ml20m_d256_train_epoch(ml20m):
+@pytest.mark.parametrize("use_snr", [False, True])
+def test_safer2_ml20m_d256_train_epoch(ml20m, use_snr):
     """configs[2]: Initialize() + one SAFER2 Train() epoch of the product's C++
     model (libfrecsys_model.so) vs the oracle's whole-model restatement, every
-    row compared (README.md:79 flags, use_snr 0)."""
+    row compared (README.md:79 flags; use_snr 0, and use_snr 1 with
+    sampling_ratio 0.1 as the bench times it: ComputeXi on N_u / 10 samples
+    drawn from the same seeded stream, safer2.h:716-742)."""
     up, uc, ip, ic = ml20m
     nu, ni = len(up) - 1, len(ip) - 1
     d = 256
@@ -109,26 +112,32 @@ def test_safer2_ml20m_d256_train_epoch(ml20m):
                  pd_iterations=1)
     users = np.repeat(np.arange(nu, dtype=np.int32), np.diff(up))
     m = fh.Model("safer2", users, uc, dim=d, stdev=0.1, seed=1, print_train_stats=False,
-                 use_snr=False, **flags)
+                 use_snr=use_snr, sampling_ratio=0.1, **flags)
     assert (m.n_users, m.n_items) == (nu, ni)
     m.initialize()
     m.train(1)
     ctx = m.context()
     U, V = ctx.get_embeddings(fh.SIDE_USER), ctx.get_embeddings(fh.SIDE_ITEM)
     mw = m.mean_weight()
+    w_gpu, l_gpu, _, xi_gpu = m.dual_state()
     m.close()
     om = O.Model(O.MODEL_SAFER2, d, nu, ni, reg=flags["l2_reg"], w=flags["uobs_weight"],
                  alpha=flags["alpha"], bandwidth=flags["bandwidth"], xi_iterations=5,
-                 pd_iterations=1, seed=1, use_snr=False)
+                 pd_iterations=1, seed=1, use_snr=use_snr, sampling_ratio=0.1)
     om.set_data(up, uc, ip, ic)
     om.initialize()
     assert om.train() == 0
     Uo, Vo = om.embeddings()
     lo, wo, xo = om.state()
     all_u, all_i = np.arange(nu), np.arange(ni)
-    _check("safer2_ml20m_d256_epoch_user", U, Uo, all_u, up)
-    _check("safer2_ml20m_d256_epoch_item", V, Vo, all_i, ip)
+    tag = "_snr" if use_snr else ""
+    _check(f"safer2_ml20m_d256_epoch{tag}_user", U, Uo, all_u, up)
+    _check(f"safer2_ml20m_d256_epoch{tag}_item", V, Vo, all_i, ip)
     assert abs(mw - float(np.mean(wo.astype(np.float64)))) < 1e-4, (mw, float(np.mean(wo)))
+    # the dual state after the epoch: losses, xi (the same seeded SNR draws)
+    np.testing.assert_allclose(l_gpu, lo, rtol=1e-4, atol=1e-7)
+    assert abs(xi_gpu - float(xo)) <= 1e-4 * max(1.0, abs(float(xo))), (xi_gpu, float(xo))
+    np.testing.assert_allclose(w_gpu, wo, rtol=0, atol=1e-4)
 
 
 @pytest.fixture(scope="module")
