@@ -176,61 +176,36 @@ def host_cpu_share():
     return share, info
 
 
-def heff_fn(model, side, quirks=True):
-    """Rows the assembly reads per entity (h, plus the ProjectV tail-quirk
-    rows of the weighted V kinds, safer2.h:196-208)."""
-    if model in ("safer2", "erm_mf", "cvar_mf") and side == fh.SIDE_ITEM and quirks:
-        return lambda h: np.where((h > 128) & (h % 128 != 0), h + 128 - h % 128, h)
-    return lambda h: h
-
-
-def path_accounting(ctx, spec, ptrs, timers, K):
-    """Algorithmic work per solve path of both half-steps."""
-    d = spec["dim"]
-    Dp = fh.padded_dim(d)
-    wide = Dp > 256
-    dual_max, split_rows = ctx.history_space_max_h(), 4096  # capi.hip split_rows default
-    chol = d ** 3 / 3.0 + 2.0 * d * d
+def path_accounting(ctx, timers, K):
+    """Algorithmic work per solve path of both half-steps, as the library
+    itself accounted it while launching (frecsys_work: SURVEY 8(d) flops and
+    bytes per entity of the paths it chose), over the HIP-event times."""
     fin_flops, fin_ms, fin_n = 0.0, 0.0, 0
     paths = {}
-    for side, ptr, name in ((fh.SIDE_USER, ptrs[0], "solve_user"),
-                            (fh.SIDE_ITEM, ptrs[1], "solve_item")):
-        lo_, hi_ = ctx.shard_range(side)
-        hs = np.diff(ptr)[lo_:hi_].astype(np.float64)
-        hs = hs[hs > 0]
-        he = heff_fn(spec["model"], side)(hs)
-        ds = he[he > dual_max] if dual_max > 0 else he
-        if wide or split_rows <= 0:
-            unsplit, split = ds, ds[:0]
-        else:
-            unsplit, split = ds[ds <= 2 * split_rows], ds[ds > 2 * split_rows]
-        f_fin = float(np.sum(unsplit) * d * (d + 1) + len(ds) * chol)
-        ms, n = timers[name + ".dspace"]
-        if n:  # per step: this side's d-space flops (one or two launches)
-            fin_flops += f_fin
+    per = lambda x: x / max(K, 1)  # noqa: E731
+    for name in ("solve_user", "solve_item"):
+        f, b, ne, n = ctx.work(name + ".dspace")
+        ms, nt = timers[name + ".dspace"]
+        if nt:
+            fin_flops += f
             fin_ms += ms
-            fin_n += n
-        hsp = he[he <= dual_max] if dual_max > 0 else he[:0]
-        hp = 32.0 * np.ceil(hsp / 32.0)
+            fin_n += nt
+        fs, _, nsplit, _ = ctx.work(name + ".split")
         sp_ms, sp_n = timers[name + ".split"]
+        fh_, _, nh, _ = ctx.work(name + ".hspace")
         hs_ms, hs_n = timers[name + ".hspace"]
         paths[name] = {
-            "dspace_entities": int(len(ds)), "dspace_ms": ms / max(K, 1),
-            "dspace_launches_per_step": n / max(K, 1),
-            "dspace_tflops": f_fin / (ms / max(K, 1) * 1e-3) / 1e12 if n else None,
-            "split_rows_total": float(np.sum(split)),
-            "split_ms": sp_ms / max(K, 1),
-            "split_tflops": (float(np.sum(split)) * d * (d + 1) / (sp_ms / sp_n * 1e-3) / 1e12)
-            if sp_n else None,
-            "hspace_entities": int(len(hsp)), "hspace_ms": hs_ms / max(K, 1),
-            # history-space algorithmic flops: h_p^2 * Dp (SYRK of S) + h_p^3 / 3
-            "hspace_tflops": (float(np.sum(hp * hp * Dp + hp ** 3 / 3.0))
-                              / (hs_ms / max(K, 1) * 1e-3) / 1e12) if hs_n else None,
-            "basis_ms": timers[name + ".basis"][0] / max(K, 1),
-            "rotate_ms": timers[name + ".rotate"][0] / max(K, 1),
+            "dspace_entities": per(ne), "dspace_ms": per(ms), "dspace_launches_per_step": per(nt),
+            "dspace_tflops": f / (ms * 1e-3) / 1e12 if nt and ms > 0 else None,
+            "split_entities": per(nsplit), "split_ms": per(sp_ms),
+            "split_tflops": fs / (sp_ms * 1e-3) / 1e12 if sp_n and sp_ms > 0 else None,
+            "hspace_entities": per(nh), "hspace_ms": per(hs_ms),
+            "hspace_tflops": fh_ / (hs_ms * 1e-3) / 1e12 if hs_n and hs_ms > 0 else None,
+            "basis_ms": per(timers[name + ".basis"][0]),
+            "rotate_ms": per(timers[name + ".rotate"][0]),
         }
     avg_ms = fin_ms / max(fin_n, 1)
-    flops = fin_flops * max(K, 1) / max(fin_n, 1)  # per launch (mean over launches)
+    flops = fin_flops / max(fin_n, 1)  # per launch (mean over launches)
     return paths, avg_ms, flops
 
 
@@ -339,11 +314,11 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
     K = steps
     d = spec["dim"]
     Dp = fh.padded_dim(d)
-    names = ["solve_user", "solve_item", "gramian", "user_loss", "allgather", "allreduce"]
+    names = ["solve_user", "solve_item", "gramian", "user_loss", "allgather", "gram_exchange"]
     names += [f"{s}.{p}" for s in ("solve_user", "solve_item")
               for p in ("dspace", "split", "basis", "hspace", "rotate")]
     timers = {k: ctx.timing(k) for k in names}
-    paths, avg_ms, flops = path_accounting(ctx, spec, (up, ip), timers, K)
+    paths, avg_ms, flops = path_accounting(ctx, timers, K)
     achieved_tf = flops / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
     ulo, uhi = ctx.shard_range(fh.SIDE_USER)
     ilo, ihi = ctx.shard_range(fh.SIDE_ITEM)
@@ -352,7 +327,8 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
     gb = gather_bytes(up, ulo, uhi, d, d) + gather_bytes(ip, ilo, ihi, d, d)
     g_gbs = gb / ((su_ms + si_ms) * 1e-3) / 1e9 if su_ms + si_ms > 0 else 0.0
     loss_ms = timers["user_loss"][0] / max(timers["user_loss"][1], 1)
-    lb = gather_bytes(up, ulo, uhi, d, 1)
+    lw = ctx.work("user_loss")
+    lb = lw[1] / max(lw[3], 1)  # algorithmic bytes per ComputeUserLoss pass (library-accounted)
     l_gbs = lb / (loss_ms * 1e-3) / 1e9 if loss_ms > 0 else 0.0
     traffic, traffic_src = load_pmc(name) if world == 1 else (None, None)
     wide = Dp > 256

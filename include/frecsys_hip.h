@@ -255,6 +255,17 @@ int frecsys_synchronize(frecsys_ctx* ctx);
 int frecsys_timing(const frecsys_ctx* ctx, const char* what, double* total_ms,
                    int64_t* launches);
 int frecsys_timing_reset(frecsys_ctx* ctx);
+/* The algorithmic work the library launched under timer key `what` since
+ * the last frecsys_timing_reset (SURVEY 8(d) definitions at the logical
+ * dim d, per entity of h assembly rows): "<solve>.dspace" h d (d+1) +
+ * d^3/3 + 2 d^2 flops (the SYRK of split entities is "<solve>.split"'s),
+ * gather bytes h d 4 + h 4 + 8 + d 4; "<solve>.hspace" h^2 d + h^3/3 +
+ * 4 h d flops, bytes 2 h d 4 + h 4 + 8 + 4 d 4; "gramian" 2 N d^2 flops over
+ * the rows this rank formed, N d 4 bytes; "user_loss" 2 nnz d + 2 N d^2
+ * flops, nnz d 4 + nnz 4 + (N+1) 8 + N 4 bytes.  `launches` counts the
+ * timed calls, as frecsys_timing does.  Any output may be NULL. */
+int frecsys_work(const frecsys_ctx* ctx, const char* what, double* flops, double* bytes,
+                 int64_t* entities, int64_t* launches);
 /* Longest assembly history (h_eff) the history-space path takes on this
  * context (0: that path is off); longer histories run the d-space solve. */
 int32_t frecsys_history_space_max_h(const frecsys_ctx* ctx);

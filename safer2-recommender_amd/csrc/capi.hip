@@ -39,6 +39,13 @@ struct Timer {
   int64_t launches = 0;
 };
 
+// Algorithmic work the library launched under a timer key (SURVEY 8(d)
+// definitions, logical dim d; frecsys_work), accumulated per launch.
+struct Work {
+  double flops = 0.0, bytes = 0.0;
+  int64_t entities = 0, launches = 0;
+};
+
 }  // namespace
 
 struct frecsys_ctx {
@@ -85,6 +92,8 @@ struct frecsys_ctx {
   int64_t err_entity = -1;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::map<std::string, Timer> timers;
+  std::map<std::string, Work> work;
+  std::map<float**, std::pair<float*, size_t>> pinned;  // upload() staging per destination
   // history-space (dual) path: a second stream for the concurrent d-space
   // solve of the long histories, the basis of each side's Gramian, the
   // rotated copy of each side, and the solved rows in the rotated basis
@@ -138,6 +147,7 @@ struct frecsys_ctx {
   float* d_slabs = nullptr;
   size_t cap_slabs = 0;
   std::vector<int32_t> order_h[3];       // history lengths in queue order
+  std::vector<QueueRec> h_order[3];      // host copy of each side's queue (source of its upload)
   int dual_on = 1;
   // Content versions (every write of a side's embeddings or Gramian takes a
   // fresh number): a Gramian recomputed from unchanged embeddings is reused
@@ -156,7 +166,7 @@ struct frecsys_ctx {
   uint64_t xrot_gram[2] = {0, 0};   // ... and the basis it was rotated into
   bool dual_used[3] = {false, false, false};  // the side's last solve took history space
   int eager_on = 1;                 // FRECSYS_EAGER=0: no early basis builds (A/B)
-  hipStream_t stream5 = nullptr;
+  hipStream_t stream5 = nullptr;  // early basis builds: an alias of stream3
   hipEvent_t ev_pre5 = nullptr;
   hipEvent_t ev_eager[2] = {nullptr, nullptr};
   bool eager_pending[2] = {false, false};
@@ -195,6 +205,22 @@ int fail(frecsys_ctx* c, int code, const std::string& msg) {
       return fail((c), FRECSYS_ERR_RCCL,                                            \
                   std::string(#expr) + ": " + ncclGetErrorString(_r));              \
   } while (0)
+
+void add_work(frecsys_ctx* c, const std::string& key, double flops, double bytes,
+              int64_t entities) {
+  Work& w = c->work[key];
+  w.flops += flops;
+  w.bytes += bytes;
+  w.entities += entities;
+  w.launches += 1;
+}
+
+// SURVEY 8(d) per entity of h assembly rows at dim d: d-space SYRK
+// h d (d+1) and LLT d^3/3 + 2 d^2 flops; gather bytes h d 4 (rows) + h 4
+// (ids) + 8 (row offset) + d 4 (the solution written).
+double dspace_syrk_flops(double h, double d) { return h * d * (d + 1.0); }
+double dspace_solve_flops(double d) { return d * d * d / 3.0 + 2.0 * d * d; }
+double gather_bytes(double h, double d) { return h * d * 4.0 + h * 4.0 + 8.0 + d * 4.0; }
 
 template <typename T>
 int ensure(frecsys_ctx* c, T** p, size_t* cap, size_t count) {
@@ -258,7 +284,8 @@ int build_order(frecsys_ctx* c, int side) {
   std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) {
     return (rp[x + 1] - rp[x]) > (rp[y + 1] - rp[y]);
   });
-  std::vector<QueueRec> recs(ord.size());
+  std::vector<QueueRec>& recs = c->h_order[side];  // lives until the next rebuild (async copy)
+  recs.resize(ord.size());
   for (size_t i = 0; i < ord.size(); ++i) {
     const int32_t e = ord[i];
     recs[i].entity = e;
@@ -290,7 +317,7 @@ int build_order(frecsys_ctx* c, int side) {
 // solve; at most max_slabs slabs of slab_floats each (longest entities first).
 int plan_split(frecsys_ctx* c, const std::vector<int32_t>& hs, int64_t n,
                const std::function<int64_t(int64_t)>& heff, SolveArgs* a, int64_t C,
-               size_t slab_floats, int64_t max_slabs) {
+               size_t slab_floats, int64_t max_slabs, hipStream_t s) {
   a->split = nullptr;
   a->n_split = 0;
   a->slabs = nullptr;
@@ -315,10 +342,14 @@ int plan_split(frecsys_ctx* c, const std::vector<int32_t>& hs, int64_t n,
   if (rc) return rc;
   rc = ensure(c, &c->d_slabs, &c->cap_slabs, (size_t)slab * slab_floats);
   if (rc) return rc;
-  HIP_TRY(c, hipMemcpy(c->d_split, c->h_split.data(), sizeof(int2) * c->h_split.size(),
-                       hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMemcpy(c->d_work, c->h_work.data(), sizeof(SplitWork) * c->h_work.size(),
-                       hipMemcpyHostToDevice));
+  // on the solve's own stream: a blocking hipMemcpy went through a queue that
+  // could be FIFO-behind the basis chain, holding the d-space launch back
+  // (h_split / h_work live in the context until the next call, after the
+  // stream has been synchronised)
+  HIP_TRY(c, hipMemcpyAsync(c->d_split, c->h_split.data(), sizeof(int2) * c->h_split.size(),
+                            hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->d_work, c->h_work.data(), sizeof(SplitWork) * c->h_work.size(),
+                            hipMemcpyHostToDevice, s));
   a->split = c->d_split;
   a->n_split = (int64_t)c->h_split.size();
   a->slabs = c->d_slabs;
@@ -383,11 +414,10 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
   }
   HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp, c->refl[other],
                             tau, s, c->tri_work));
-  HIP_TRY(c, launch_form_q(c->refl[other], tau, Dp, c->q[other], s));
-  for (int t = 0; t < 2; ++t) {  // bf16-piece images of Q (forward) and Q^T (back)
+  for (int t = 0; t < 2; ++t)  // bf16-piece images of Q (forward) and Q^T (back)
     if (!c->qsplit[other][t]) HIP_TRY(c, hipMalloc(&c->qsplit[other][t], basis_split_bytes(Dp)));
-    HIP_TRY(c, launch_split_basis(c->q[other], Dp, t, c->qsplit[other][t], s));
-  }
+  HIP_TRY(c, launch_form_q(c->refl[other], tau, Dp, c->q[other], s, c->qsplit[other][0],
+                           c->qsplit[other][1]));
   HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp, s));
   return FRECSYS_OK;
 }
@@ -428,10 +458,26 @@ int allgather_rows(frecsys_ctx* c, float* base, int side, int64_t ld) {
   return FRECSYS_OK;
 }
 
+// Host -> device upload of a per-entity vector through a pinned staging
+// buffer of its own (one per destination): a DMA the stream orders like a
+// kernel, instead of a pageable-memory copy that the runtime stages itself
+// (observed waiting for work queued on other streams).  Every call that
+// uploads synchronises its stream before returning, so a staging buffer is
+// never rewritten while its copy is in flight.
 int upload(frecsys_ctx* c, float** dptr, size_t* cap, const float* host, size_t n) {
   int rc = ensure(c, dptr, cap, n);
   if (rc) return rc;
-  HIP_TRY(c, hipMemcpyAsync(*dptr, host, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+  auto& pin = c->pinned[dptr];
+  if (pin.second < n) {
+    if (pin.first) HIP_TRY(c, hipHostFree(pin.first));
+    pin.first = nullptr;
+    pin.second = 0;
+    HIP_TRY(c, hipHostMalloc((void**)&pin.first, sizeof(float) * std::max<size_t>(n, 1),
+                             hipHostMallocDefault));
+    pin.second = n;
+  }
+  if (n) std::memcpy(pin.first, host, sizeof(float) * n);
+  HIP_TRY(c, hipMemcpyAsync(*dptr, pin.first, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
   return FRECSYS_OK;
 }
 
@@ -535,6 +581,12 @@ int form_gramian(frecsys_ctx* c, int slot, const float* X, int64_t n, const floa
   g.g_lo = g_lo;
   g.g_hi = g_hi;
   HIP_TRY(c, launch_gramian(c->Dp, g, c->stream));
+  if (slot < 2 && g_hi > g_lo) {  // 2 N d^2 over the rows of the groups formed here
+    const int64_t r0 = gram_group_leaf(pl, g_lo) * pl.rpl;
+    const int64_t r1 = std::min<int64_t>(n, gram_group_leaf(pl, g_hi) * pl.rpl);
+    const double rows = (double)(r1 - r0), dd = c->dim;
+    add_work(c, "gramian", 2.0 * rows * dd * dd, rows * dd * 4.0, r1 - r0);
+  }
   if (!all_groups && c->comm) {
     const size_t k = ktimer_begin(c, "gram_exchange", c->stream);
     rc = allgather_groups(c, c->d_gslabs[slot], pl);
@@ -721,11 +773,17 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
       hipEventCreateWithFlags(&c->ev_fork3, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join3, hipEventDisableTiming) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed (stream2/3)"));
-  if (hipStreamCreateWithFlags(&c->stream5, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_pre5, hipEventDisableTiming) != hipSuccess ||
+  // the early basis builds share stream3 with the second bucket lane: with
+  // GPU_MAX_HW_QUEUES = 4 a fifth stream shared a hardware queue with the
+  // d-space stream, whose solve then waited (in FIFO order) for the whole
+  // basis chain queued before it -- 0.5 ms per ML-20M epoch.  stream3 is idle
+  // when a Gramian triggers an early build, and the buckets it runs later
+  // need that basis anyway.
+  c->stream5 = c->stream3;
+  if (hipEventCreateWithFlags(&c->ev_pre5, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_eager[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_eager[1], hipEventDisableTiming) != hipSuccess)
-    return bail(fail(c, FRECSYS_ERR_HIP, "hipStreamCreate failed (stream5)"));
+    return bail(fail(c, FRECSYS_ERR_HIP, "hipEventCreate failed (early builds)"));
   if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
   if (const char* v = getenv("FRECSYS_EAGER")) c->eager_on = atoi(v);
   // d-space / history-space crossover: by flops h = d, but at Dp <= 256 the
@@ -816,6 +874,8 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (c->d_split) (void)hipFree(c->d_split);
   if (c->d_work) (void)hipFree(c->d_work);
   if (c->d_slabs) (void)hipFree(c->d_slabs);
+  for (auto& kv : c->pinned)
+    if (kv.second.first) (void)hipHostFree(kv.second.first);
   for (auto& p : c->pending) c->event_pool.insert(c->event_pool.end(), {p.a, p.b});
   for (hipEvent_t e : c->event_pool) (void)hipEventDestroy(e);
   if (c->ev_fork3) (void)hipEventDestroy(c->ev_fork3);
@@ -832,7 +892,7 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   }
   for (hipEvent_t e : {c->ev_pre5, c->ev_eager[0], c->ev_eager[1]})
     if (e) (void)hipEventDestroy(e);
-  if (c->stream5) (void)hipStreamDestroy(c->stream5);
+  c->stream5 = nullptr;  // = stream3, destroyed above
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1147,17 +1207,27 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
     if (can_split) {  // long histories of the first batch cut into slabs (a budget of their own)
       const size_t sf = wide_slab_floats(c->Dp);
       rc = plan_split(c, hs, batch, heff, &ap, wide_slab_rows(), sf,
-                      (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (sf * sizeof(float))));
+                      (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (sf * sizeof(float))), s);
       if (rc) return rc;
     }
     const size_t k = ktimer_begin(c, pre + ".dspace", s);
     HIP_TRY(c, launch_wide_solve(c->Dp, ap, c->wide_ws, batch, s));
     ktimer_end(c, k, s);
+    double f = 0, b = 0;
+    int64_t ne = 0;
+    for (int64_t i = 0; i < ap.n_rows; ++i) {
+      const double h = (double)heff(hs[i]);
+      if (h <= 0) continue;  // untouched
+      f += dspace_syrk_flops(h, c->dim) + dspace_solve_flops(c->dim);
+      b += gather_bytes(h, c->dim);
+      ++ne;
+    }
+    add_work(c, pre + ".dspace", f, b, ne);  // slabs + batches: one timed call
     return FRECSYS_OK;
   }
   if (can_split) {
     int rc = plan_split(c, hs, ap.n_rows, heff, &ap, c->split_rows, split_slab_floats(c->Dp),
-                        INT64_MAX);
+                        INT64_MAX, s);
     if (rc) return rc;
   }
   if (ap.n_work > 0) {
@@ -1175,6 +1245,27 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
   const size_t k = ktimer_begin(c, pre + ".dspace", s);
   HIP_TRY(c, launch_solve(c->Dp, ap, s));
   ktimer_end(c, k, s);
+  {  // the split entities' SYRK is the split kernel's work, their solve this one's
+    double f = 0, b = 0, fs = 0, bs = 0;
+    int64_t ne = 0, nsplit = 0;
+    for (int64_t i = 0; i < ap.n_rows; ++i) {
+      const double h = (double)heff(hs[i]);
+      if (h <= 0) continue;
+      ++ne;
+      if (i < ap.n_split) {
+        fs += dspace_syrk_flops(h, c->dim);
+        bs += h * c->dim * 4.0 + h * 4.0;
+        f += dspace_solve_flops(c->dim);
+        b += 8.0 + c->dim * 4.0;
+        ++nsplit;
+      } else {
+        f += dspace_syrk_flops(h, c->dim) + dspace_solve_flops(c->dim);
+        b += gather_bytes(h, c->dim);
+      }
+    }
+    add_work(c, pre + ".dspace", f, b, ne);
+    if (ap.n_work > 0) add_work(c, pre + ".split", fs, bs, nsplit);
+  }
   if (dprof) {  // diagnostics: mean cycles per entity and phase
     unsigned long long hp[16];
     HIP_TRY(c, hipStreamSynchronize(s));
@@ -1258,7 +1349,10 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
   a.n_work = 0;
   a.debug_skip = c->debug_skip;
   const unsigned long long none = ~0ull;
-  HIP_TRY(c, hipMemcpyAsync(c->d_fail, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
+  // ~0ull by a device-side fill: an H2D copy from host memory at this point
+  // was observed starting only after the early basis build queued on another
+  // stream had finished, holding back the fork of the d-space solve
+  HIP_TRY(c, hipMemsetAsync(c->d_fail, 0xFF, sizeof(none), c->stream));
   // Queue split: the queue is sorted by decreasing history, and h_eff (the
   // rows the assembly reads, tail-quirk rows included) is monotone in h, so
   // the d-space entities are a prefix, then the history-space buckets
@@ -1383,6 +1477,17 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       d.pos0 = 0;
       HIP_TRY(c, launch_dual_sweep(d, c->stream));
       ktimer_end(c, k, c->stream);
+      {  // h x h system per entity: S = I + Z D^-1 Z^T (h^2 d), its LLT (h^3 / 3),
+         // the recurrence and Y^T z (4 h d); rows read twice, the LDL row
+        double f = 0, b = 0;
+        const double dd = c->dim;
+        for (int64_t i = n_dspace; i < n_nonempty; ++i) {
+          const double h = (double)heff(hs[i]);
+          f += h * h * dd + h * h * h / 3.0 + 4.0 * h * dd;
+          b += 2.0 * h * dd * 4.0 + h * 4.0 + 8.0 + 3.0 * dd * 4.0 + dd * 4.0;
+        }
+        add_work(c, pre + ".hspace", f, b, n_nonempty - n_dspace);
+      }
       k = ktimer_begin(c, pre + ".rotate", c->stream);
       HIP_TRY(c, launch_rotate(c->out_rot[side], a.order + n_dspace, 0, n_nonempty - n_dspace,
                                c->qsplit[other][1], a.out, c->Dp, c->stream, 1));
@@ -1478,6 +1583,13 @@ int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, fl
     ScopedTimer t(c, "user_loss");
     HIP_TRY(c, launch_user_loss(c->Dp, a, c->stream));
     t.stop();
+  }
+  if (side == 0) {  // gather of the item rows + u^T G u: SURVEY 8(d) bytes with a 1-float output
+    const std::vector<int64_t>& rp = c->host_rp[0];
+    const double nnz = rp.empty() ? 0.0 : (double)(rp[hi] - rp[lo]), n = (double)(hi - lo);
+    const double dd = c->dim;
+    add_work(c, "user_loss", 2.0 * nnz * dd + 2.0 * n * dd * dd,
+             nnz * dd * 4.0 + nnz * 4.0 + (n + 1.0) * 8.0 + n * 4.0, hi - lo);
   }
   if (host_out) {
     if (side == 0 && (c->world > 1 || c->comm)) {
@@ -1636,7 +1748,10 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
   a.other_weight = kind == FRECSYS_KIND_WEIGHTED_V ? c->d_other_weight : nullptr;
   a.resid = c->d_resid;
   const unsigned long long none = ~0ull;
-  HIP_TRY(c, hipMemcpyAsync(c->d_fail, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
+  // ~0ull by a device-side fill: an H2D copy from host memory at this point
+  // was observed starting only after the early basis build queued on another
+  // stream had finished, holding back the fork of the d-space solve
+  HIP_TRY(c, hipMemsetAsync(c->d_fail, 0xFF, sizeof(none), c->stream));
   {
     ScopedTimer t(c, "pp_step");
     HIP_TRY(c, launch_pp_step(a, c->stream));
@@ -1736,6 +1851,18 @@ int frecsys_timing(const frecsys_ctx* c, const char* what, double* total_ms, int
   return FRECSYS_OK;
 }
 
+int frecsys_work(const frecsys_ctx* c, const char* what, double* flops, double* bytes,
+                 int64_t* entities, int64_t* launches) {
+  if (!c || !what) return FRECSYS_ERR_INVALID;
+  auto it = c->work.find(what);
+  const Work w = it == c->work.end() ? Work{} : it->second;
+  if (flops) *flops = w.flops;
+  if (bytes) *bytes = w.bytes;
+  if (entities) *entities = w.entities;
+  if (launches) *launches = w.launches;
+  return FRECSYS_OK;
+}
+
 int frecsys_debug_diag_factor(frecsys_ctx* c, int32_t blocked, int32_t n_tiles, const float* a,
                               float* linv, int32_t* ok) {
   if (!c || n_tiles < 0 || (n_tiles && (!a || !linv || !ok)))
@@ -1785,6 +1912,7 @@ int32_t frecsys_history_space_max_h(const frecsys_ctx* c) {
 int frecsys_timing_reset(frecsys_ctx* c) {
   if (!c) return FRECSYS_ERR_INVALID;
   c->timers.clear();
+  c->work.clear();
   return FRECSYS_OK;
 }
 

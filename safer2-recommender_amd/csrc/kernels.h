@@ -170,8 +170,11 @@ hipError_t launch_dual(int tiles, const DualArgs& a, hipStream_t s);
 // entries k+1..Dp-1) and their tau.
 hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
                           float* tau, hipStream_t s, float* work = nullptr);
-// Q = H_0 H_1 ... H_{Dp-3} from the reflectors, row-major Dp x Dp.
-hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s);
+// Q = H_0 H_1 ... H_{Dp-3} from the reflectors, row-major Dp x Dp; with
+// img_q / img_qt also the split images of Q and Q^T (launch_split_basis's
+// layout, basis_split_bytes each; Dp a multiple of 32).
+hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s,
+                         void* img_q = nullptr, void* img_qt = nullptr);
 // The split image of B = (trans ? Q^T : Q) for launch_rotate: Dp * Dp * 3
 // bf16 (16-B granules in MFMA fragment order).
 size_t basis_split_bytes(int Dp);

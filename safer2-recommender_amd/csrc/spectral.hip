@@ -310,17 +310,24 @@ __global__ void __launch_bounds__(512)
 // Q = H_0 H_1 ... H_{n-3}: one wave per column c of Q, q = H_0 (H_1 (...
 // H_{n-3} e_c)); H_k leaves columns c <= k alone, so the product starts at
 // k = min(c-1, n-3).  The reflectors are staged through LDS FQ_KB at a time
-// by all 8 waves of the workgroup (one coalesced load per block instead of a
-// dependent L2 round trip per reflector), then applied from LDS.
+// by all 8 waves of the workgroup, the next block's loads issued into
+// registers before the current block is applied (one memory round trip per
+// block would otherwise sit on the chain: 16 per basis at n = 256), then
+// applied from LDS.  The epilogue writes Q and, from the 8 columns staged in
+// LDS, this workgroup's granules of the split images of Q and Q^T that the
+// rotations read (split_basis_kernel's layout; no separate launches).
 // RPL = rows per lane (n <= 64 * RPL).
 constexpr int FQ_KB = 16;
 template <int RPL>
 __global__ void __launch_bounds__(512)
-    form_q_kernel(const float* __restrict__ Vh, const float* __restrict__ tau, int n, float* Q) {
-  __shared__ __attribute__((aligned(16))) float vsh[FQ_KB][64 * RPL];
+    form_q_kernel(const float* __restrict__ Vh, const float* __restrict__ tau, int n, float* Q,
+                  bf16x8* __restrict__ img_q, bf16x8* __restrict__ img_qt) {
+  constexpr int ROWS = 64 * RPL;
+  constexpr int PER = FQ_KB * ROWS / 512;  // staged values per thread and block
+  __shared__ __attribute__((aligned(16))) float vsh[FQ_KB][ROWS];
   __shared__ float tsh[FQ_KB];
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 8 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 8 + wave;
   const int c_first = blockIdx.x * 8;
   float q[RPL];
 #pragma unroll
@@ -329,14 +336,30 @@ __global__ void __launch_bounds__(512)
   // highest reflector any column of this workgroup needs
   int ktop = c_first + 7 - 1 < n - 3 ? c_first + 7 - 1 : n - 3;
   if (ktop >= n) ktop = n - 1;
-  for (int kb = ktop - (ktop % FQ_KB); kb >= 0; kb -= FQ_KB) {
-    __syncthreads();  // previous block consumed
-    for (int s = threadIdx.x; s < FQ_KB * 64 * RPL; s += 512) {
-      const int kk = kb + s / (64 * RPL), row = s % (64 * RPL);
-      vsh[s / (64 * RPL)][row] = (kk <= ktop && row > kk && row < n) ? Vh[(int64_t)kk * n + row] : 0.0f;
+  float pre[PER];
+  float tpre = 0.0f;
+  auto fetch = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int s2 = threadIdx.x + 512 * i;
+      const int kk = kb + s2 / ROWS, row = s2 % ROWS;
+      pre[i] = (kb >= 0 && kk <= ktop && row > kk && row < n) ? Vh[(int64_t)kk * n + row] : 0.0f;
     }
-    if (threadIdx.x < FQ_KB) tsh[threadIdx.x] = kb + (int)threadIdx.x <= ktop ? tau[kb + threadIdx.x] : 0.0f;
+    if (threadIdx.x < FQ_KB)
+      tpre = (kb >= 0 && kb + (int)threadIdx.x <= ktop) ? tau[kb + threadIdx.x] : 0.0f;
+  };
+  const int kb0 = ktop >= 0 ? ktop - (ktop % FQ_KB) : -1;
+  if (kb0 >= 0) fetch(kb0);
+  for (int kb = kb0; kb >= 0; kb -= FQ_KB) {
+    __syncthreads();  // previous block consumed
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int s2 = threadIdx.x + 512 * i;
+      vsh[s2 / ROWS][s2 % ROWS] = pre[i];
+    }
+    if (threadIdx.x < FQ_KB) tsh[threadIdx.x] = tpre;
     __syncthreads();
+    if (kb - FQ_KB >= 0) fetch(kb - FQ_KB);  // in flight while this block is applied
     for (int j = FQ_KB - 1; j >= 0; --j) {
       const int k = kb + j;
       if (k > kstart) continue;  // wave-uniform
@@ -350,11 +373,51 @@ __global__ void __launch_bounds__(512)
       for (int r = 0; r < RPL; ++r) q[r] -= d * vsh[j][lane + 64 * r];
     }
   }
-  if (c >= n) return;
+  if (c < n) {
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const int row = lane + 64 * r;
+      if (row < n) Q[(int64_t)row * n + c] = q[r];
+    }
+  }
+  if (!img_q) return;
+  // split images (n a multiple of 32, so all 8 columns exist): the columns
+  // through LDS, [8][n]
+  __syncthreads();
+  float* qs = &vsh[0][0];
 #pragma unroll
   for (int r = 0; r < RPL; ++r) {
     const int row = lane + 64 * r;
-    if (row < n) Q[(int64_t)row * n + c] = q[r];
+    if (row < n) qs[wave * n + row] = q[r];
+  }
+  __syncthreads();
+  const int NCT = n / 32;
+  {  // image of Q: granule (s, hi) of column c = rows 16 s + 8 hi .. + 7
+    const int C = c >> 5, lo = c & 31;
+    for (int gi = lane; gi < n / 8; gi += 64) {
+      const int sg = gi >> 1, hi = gi & 1;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = qs[wave * n + 16 * sg + 8 * hi + j];
+      bf16x8 f[3];
+      split3x8(v, f);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) img_q[((int64_t)(sg * NCT + C) * 3 + p) * 64 + 32 * hi + lo] = f[p];
+    }
+  }
+  {  // image of Q^T: B[k][col] = Q[col][k], k = c_first .. c_first + 7 = one granule row
+    const int sg = c_first >> 4, hi = (c_first >> 3) & 1;
+    for (int col = threadIdx.x; col < n; col += 512) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = qs[j * n + col];
+      bf16x8 f[3];
+      split3x8(v, f);
+      const int C = col >> 5, lo = col & 31;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        img_qt[((int64_t)(sg * NCT + C) * 3 + p) * 64 + 32 * hi + lo] = f[p];
+    }
   }
 }
 
@@ -527,15 +590,20 @@ hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, flo
   return hipGetLastError();
 }
 
-hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s) {
+hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hipStream_t s,
+                         void* img_q, void* img_qt) {
   if (Dp < 4 || Dp > 1024) return hipErrorInvalidValue;
+  if ((img_q != nullptr) != (img_qt != nullptr) || (img_q && (Dp < 64 || Dp % 32)))
+    return hipErrorInvalidValue;
   const dim3 grid((unsigned)((Dp + 7) / 8));
+  bf16x8* a = reinterpret_cast<bf16x8*>(img_q);
+  bf16x8* b = reinterpret_cast<bf16x8*>(img_qt);
   if (Dp <= 256)
-    hipLaunchKernelGGL(form_q_kernel<4>, grid, dim3(512), 0, s, Vh, tau, Dp, Q);
+    hipLaunchKernelGGL(form_q_kernel<4>, grid, dim3(512), 0, s, Vh, tau, Dp, Q, a, b);
   else if (Dp <= 512)
-    hipLaunchKernelGGL(form_q_kernel<8>, grid, dim3(512), 0, s, Vh, tau, Dp, Q);
+    hipLaunchKernelGGL(form_q_kernel<8>, grid, dim3(512), 0, s, Vh, tau, Dp, Q, a, b);
   else
-    hipLaunchKernelGGL(form_q_kernel<16>, grid, dim3(512), 0, s, Vh, tau, Dp, Q);
+    hipLaunchKernelGGL(form_q_kernel<16>, grid, dim3(512), 0, s, Vh, tau, Dp, Q, a, b);
   return hipGetLastError();
 }
 

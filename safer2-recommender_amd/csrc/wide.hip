@@ -950,6 +950,178 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// The same Householder sequence as tridiag_step_kernel in ONE launch: N/16
+// persistent workgroups, each keeping its 16-column strip of the matrix in
+// registers through all N steps.  Per step a workgroup reads p_{k-1} and
+// row k of the matrix (pending update k-1 not yet applied) from a ping-pong
+// exchange buffer, forms K, w_{k-1} and reflector k redundantly (every
+// workgroup, as the step kernel does), applies update k-1 to its strip,
+// publishes its slice of p_k = tau_k A v_k and its entries of row k+1, and
+// meets the others at one grid barrier (a device-scope counter).  The strip
+// never leaves the registers (the step kernel re-read and re-wrote the whole
+// matrix per launch) and the host enqueues one launch instead of N (the
+// d-space launch queued behind them waited for the enqueue).  Arithmetic,
+// thread mapping and reduction orders are the step kernel's: bit-identical.
+// The grid (32 / 64 workgroups of 256 threads) is far below one workgroup
+// per CU, so every workgroup becomes resident even beside other kernels; a
+// bounded wait sets *err instead of spinning forever.
+__device__ __forceinline__ float xload(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xstore(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int N>
+__global__ void __launch_bounds__(256)
+    tridiag_persist_kernel(const float* __restrict__ G, float* xbuf, unsigned* bar, int* err,
+                           float* __restrict__ Vh, float* __restrict__ tau,
+                           float* __restrict__ tdiag, float* __restrict__ toff) {
+  constexpr int n = N, CW = 16, NR = N / 16, NV = N / 256, NWG = N / CW;
+  const int c0 = blockIdx.x * CW;
+  const int tid = threadIdx.x;
+  const int c = c0 + (tid & (CW - 1)), rg = tid >> 4;
+  const bool writer = blockIdx.x == NWG - 1;  // its columns stay live to the end
+  __shared__ float vp[N], wv[N], vk[N];
+  __shared__ float red[8];
+  __shared__ float pc[16][CW + 1];
+  __shared__ float tsh;
+  float sreg[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) sreg[i] = G[(int64_t)(rg + 16 * i) * n + c];
+  for (int r = tid; r < N; r += 256) vp[r] = 0.0f;
+  if (tid == 0) tsh = 0.0f;
+  __syncthreads();
+  for (int k = 0; k < n; ++k) {
+    const bool live = c0 + CW > k + 1 || writer;  // workgroup-uniform
+    float* pin = xbuf + (size_t)(k & 1) * 2 * N;
+    float* pout = xbuf + (size_t)((k + 1) & 1) * 2 * N;
+    if (live) {
+      const float tp = tsh;
+      float pir[NV], akr[NV];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int r = tid + 256 * j;
+        pir[j] = (k > 0 && r >= k) ? xload(pin + r) : 0.0f;
+        akr[j] = r >= k ? (k == 0 ? G[r] : xload(pin + N + r)) : 0.0f;
+      }
+      float d = 0.0f;
+      if (tp != 0.0f) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) d += pir[j] * vp[tid + 256 * j];
+      }
+      d = block_sum(d, red);
+      const float K = -0.5f * tp * d;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int r = tid + 256 * j;
+        wv[r] = (tp != 0.0f && r >= k) ? pir[j] + K * vp[r] : 0.0f;
+      }
+      __syncthreads();
+      const float vpk = vp[k], wk = wv[k];
+      float xn = 0.0f;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int r = tid + 256 * j;
+        if (r >= k) {
+          const float ck = akr[j] - vpk * wv[r] - wk * vp[r];
+          vk[r] = ck;
+          if (r >= k + 2) xn += ck * ck;
+        }
+      }
+      xn = block_sum(xn, red);
+      const float dkk = vk[k];
+      float beta = 0.0f, tk = 0.0f, scal = 0.0f;
+      if (k + 1 < n) {
+        const float alpha = vk[k + 1];
+        if (xn == 0.0f) {
+          beta = alpha;
+          tk = 0.0f;
+        } else {
+          beta = -copysignf(sqrtf(alpha * alpha + xn), alpha);
+          tk = (beta - alpha) / beta;
+          scal = 1.0f / (alpha - beta);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int r = tid + 256 * j;
+        float v = 0.0f;
+        if (r == k + 1) v = 1.0f;
+        else if (r >= k + 2) v = tk != 0.0f ? vk[r] * scal : 0.0f;
+        vk[r] = v;
+      }
+      __syncthreads();
+      if (writer) {
+        if (tid == 0) {
+          tdiag[k] = dkk;
+          toff[k] = k + 1 < n ? beta : 0.0f;
+          tau[k] = tk;
+        }
+        if (k + 1 < n)
+          for (int r = k + 1 + tid; r < n; r += 256) Vh[(int64_t)k * n + r] = vk[r];
+      }
+      if (k + 1 >= n) break;  // the last step: no update, no exchange (every workgroup)
+      // finish update k-1 on my columns (rows >= k+1), p_k partials, row k+1
+      const bool col_live = c >= k + 1 && c < n;
+      float pacc = 0.0f;
+      if (col_live) {
+        const float vpc = vp[c], wc = wv[c];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const int r = rg + 16 * i;
+          if (r >= k + 1) {
+            const float v = sreg[i] - vp[r] * wc - wv[r] * vpc;
+            sreg[i] = v;
+            pacc += v * vk[r];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+          if (rg + 16 * i == k + 1) xstore(pout + N + c, sreg[i]);  // row k+1, my column
+      }
+      pc[rg][tid & (CW - 1)] = pacc;
+      __syncthreads();
+      if (tid < CW) {
+        const int cc = c0 + tid;
+        float sum = 0.0f;
+#pragma unroll
+        for (int g2 = 0; g2 < 16; ++g2) sum += pc[g2][tid];
+        if (cc >= k + 1 && cc < n) xstore(pout + cc, tk * sum);
+      }
+      // reflector k becomes the pending one
+      for (int r = tid; r < N; r += 256) vp[r] = vk[r];
+      if (tid == 0) tsh = tk;
+    } else if (k + 1 >= n) {
+      break;
+    }
+    // grid barrier (step k): the exchange stores above are complete and
+    // visible (release) before the arrival; reads after it see them (acquire)
+    __syncthreads();
+    if (tid == 0) {
+      __threadfence();
+      atomicAdd(bar, 1u);
+      const unsigned target = (unsigned)(k + 1) * NWG;
+      unsigned spins = 0;
+      while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 22) ||
+            __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          atomicExch(err, 1);
+          break;
+        }
+      }
+      __threadfence();
+    }
+    __syncthreads();
+  }
+  // a timed-out barrier leaves a garbage basis: poison it so that every LDL
+  // pivot of the history-space solve fails and the call reruns in d-space
+  if (writer && tid == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    tdiag[0] = __builtin_nanf("");
+}
+
 // User loss at wide Dp: one wave per user, Dp/32 lanes per history row
 // (8 float4 each), 64*32/Dp rows in flight; u^T G u from the rotate_kernel
 // partials (one per 128-column block) summed in column-block order.
@@ -1104,11 +1276,32 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
   return hipGetLastError();
 }
 
+// persistent kernel: exchange [2][2][Dp] + barrier counter + error flag; the
+// step kernels (FRECSYS_TRIDIAG_STEPS=1, A/B): two Dp x Dp copies + two p
 size_t wide_tridiag_work_floats(int Dp) { return (size_t)2 * Dp * Dp + 2 * (size_t)Dp; }
+
+bool tridiag_steps() {
+  const char* v = getenv("FRECSYS_TRIDIAG_STEPS");
+  return v && atoi(v) != 0;
+}
 
 hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
                                float* tau, float* work, hipStream_t s) {
   if (!wide_dim(Dp) || !work) return hipErrorInvalidValue;
+  if (!tridiag_steps()) {
+    float* xbuf = work;                                     // [2][2][Dp]
+    unsigned* bar = reinterpret_cast<unsigned*>(work + 4 * (size_t)Dp);
+    int* err = reinterpret_cast<int*>(work + 4 * (size_t)Dp + 1);
+    hipError_t e = hipMemsetAsync(bar, 0, 2 * sizeof(float), s);
+    if (e != hipSuccess) return e;
+    if (Dp == 512)
+      hipLaunchKernelGGL(tridiag_persist_kernel<512>, dim3(512 / 16), dim3(256), 0, s, G, xbuf, bar,
+                         err, Vh, tau, tdiag, toff);
+    else
+      hipLaunchKernelGGL(tridiag_persist_kernel<1024>, dim3(1024 / 16), dim3(256), 0, s, G, xbuf,
+                         bar, err, Vh, tau, tdiag, toff);
+    return hipGetLastError();
+  }
   const int n = Dp;
   float* A[2] = {work, work + (size_t)n * n};
   float* P[2] = {work + (size_t)2 * n * n, work + (size_t)2 * n * n + n};

@@ -39,7 +39,7 @@ EXPORTS = (
     "frecsys_pp_predict", "frecsys_pp_step", "frecsys_debug_diag_factor",
     "frecsys_history_space_max_h", "frecsys_comm_world", "frecsys_gram_groups",
     "frecsys_get_gram_groups", "frecsys_set_gram_groups", "frecsys_get_gramian",
-    "frecsys_gram_plan",
+    "frecsys_gram_plan", "frecsys_work",
 )
 
 # Every symbol include/frecsys_model.h declares.
@@ -130,6 +130,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_set_gram_groups": (ctypes.c_int, [P, I32, P]),
         "frecsys_get_gramian": (ctypes.c_int, [P, I32, P, I64]),
         "frecsys_gram_plan": (ctypes.c_int, [I32, I64, I32, I32, P, P, P, P, P]),
+        "frecsys_work": (ctypes.c_int, [P, ctypes.c_char_p, P, P, P, P]),
         "frecsys_debug_basis": (ctypes.c_int, [P, I32, P, P, P]),
         "frecsys_debug_diag_factor": (ctypes.c_int, [P, I32, I32, P, P, P]),
         "frecsys_eval_topk": (ctypes.c_int, [P, I32, P]),
@@ -377,6 +378,15 @@ class Context:
         self._check(self.lib.frecsys_timing(self.h, what.encode(), ctypes.byref(ms),
                                             ctypes.byref(n)))
         return float(ms.value), int(n.value)
+
+    def work(self, what: str):
+        """(flops, bytes, entities, launches) of timer key `what`: the
+        algorithmic work the library launched (frecsys_work)."""
+        f, b = ctypes.c_double(), ctypes.c_double()
+        e, n = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.frecsys_work(self.h, what.encode(), ctypes.byref(f), ctypes.byref(b),
+                                          ctypes.byref(e), ctypes.byref(n)))
+        return float(f.value), float(b.value), int(e.value), int(n.value)
 
     def history_space_max_h(self) -> int:
         return int(self.lib.frecsys_history_space_max_h(self.h))
