@@ -218,17 +218,55 @@ def gather_bytes(ptr, lo, hi, d, out_floats):
 
 
 def load_pmc(workload):
+    """The workload's counter summary in profiles/latest_pmc.json (rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes, scripts/profile_round.sh), or {}."""
     path = os.path.join(ROOT, "profiles", "latest_pmc.json")
     if not os.path.exists(path):
-        return None, None
+        return {}, None
     try:
         js = json.load(open(path))
     except (OSError, ValueError):
-        return None, None
-    w = js.get("workloads", {}).get(workload)
-    if not w:
-        return None, None
-    return w.get("dominant_traffic_bytes"), js.get("source")
+        return {}, None
+    return js.get("workloads", {}).get(workload, {}), js.get("source")
+
+
+def loss_roofline(pmc, alg_bytes, ms, alg_gbs, table_bytes):
+    """ComputeUserLoss, a pure gather of item rows.  `achieved` is the FABRIC
+    rate: FETCH_SIZE x 2 + WRITE_SIZE bytes of its gather kernel per pass
+    (counters of the tracked profile, L2 misses incl. Infinity-Cache hits)
+    over this run's pass time.  The algorithmic rate (SURVEY 8(d) bytes over
+    time) is kept beside it; it exceeds the HBM peak whenever the item table
+    is served from the caches, so it is never called HBM."""
+    fab = pmc.get("loss_fabric_bytes_per_pass")
+    out = {"bound": "hbm", "kind": "fabric (L2-miss incl. Infinity Cache)",
+           "scope": "ComputeUserLoss gather kernel (loss_gather*)",
+           "achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": None,
+           "traffic": fab, "algorithmic_gbs": alg_gbs, "algorithmic_frac": alg_gbs / PEAK_HBM_GBS,
+           "algorithmic_bytes_per_launch": alg_bytes, "gathered_table_bytes": table_bytes}
+    if fab and ms > 0:
+        out["achieved"] = fab / (ms * 1e-3) / 1e9
+        out["frac"] = out["achieved"] / PEAK_HBM_GBS
+    return out
+
+
+def item_gather_fabric(pmc, ms, n_items, Dp):
+    """The north-star figure on a table larger than the 256 MiB Infinity
+    Cache (MSD: the item half-step gathers the 0.97 GB user table): fabric
+    bytes of every kernel of one item half-step (scripts/gather_prof.sh:
+    marker-bracketed rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes) over this
+    run's item half-step time, against 8 TB/s."""
+    h = pmc.get("halfstep_item")
+    if not h or ms <= 0:
+        return None
+    fab = h["fabric_bytes"]
+    return {"bound": "hbm", "kind": "fabric (L2-miss incl. Infinity Cache)",
+            "scope": "item half-step, every kernel (gather + workspace traffic)",
+            "gathered_table_bytes": h["gathered_table_bytes"],
+            "achieved": fab / (ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": fab / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": fab,
+            "algorithmic_gather_bytes": h["algorithmic_gather_bytes"],
+            "algorithmic_gbs": h["algorithmic_gather_bytes"] / (ms * 1e-3) / 1e9,
+            "halfstep_ms": ms}
 
 
 def cpu_baseline(spec, up, uc, V, seconds, nthreads, host):
@@ -330,7 +368,8 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
     lw = ctx.work("user_loss")
     lb = lw[1] / max(lw[3], 1)  # algorithmic bytes per ComputeUserLoss pass (library-accounted)
     l_gbs = lb / (loss_ms * 1e-3) / 1e9 if loss_ms > 0 else 0.0
-    traffic, traffic_src = load_pmc(name) if world == 1 else (None, None)
+    pmc, traffic_src = load_pmc(name) if world == 1 else ({}, None)
+    traffic = pmc.get("dominant_traffic_bytes")
     wide = Dp > 256
     res = {
         "workload": name,
@@ -354,15 +393,18 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
                      "traffic_source": traffic_src,
                      "avg_launch_ms": avg_ms, "flops_per_launch": flops},
         "paths": paths,
-        "gather_roofline": {"bound": "hbm", "scope": "both half-steps' solves (SURVEY 8(d) "
-                                                     "gather bytes / solve time)",
+        # ALGORITHMIC bytes over time: the solve phase is compute-bound (DESIGN
+        # 3.7), so this is a work rate, not a measure of HBM traffic
+        "gather_roofline": {"bound": "hbm", "kind": "algorithmic",
+                            "scope": "both half-steps' solves (SURVEY 8(d) gather bytes / solve "
+                                     "time)",
                             "achieved": g_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": g_gbs / PEAK_HBM_GBS, "bytes_per_step": gb},
-        "loss_gather_roofline": {"bound": "hbm", "scope": "ComputeUserLoss pass (loss_gather + "
-                                                          "quad kernels)",
-                                 "achieved": l_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                 "frac": l_gbs / PEAK_HBM_GBS, "bytes_per_launch": lb},
+        "loss_gather_roofline": loss_roofline(pmc, lb, loss_ms, l_gbs, ni * Dp * 4),
     }
+    item = item_gather_fabric(pmc, si_ms, ni, Dp)
+    if item:
+        res["item_gather_fabric"] = item
     if spec["model"] != "ials":
         res["mean_dual_weight"] = model.mean_weight()
     if cpu_s > 0 and world == 1 and rank == 0:

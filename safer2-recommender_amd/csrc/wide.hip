@@ -976,7 +976,7 @@ template <int N>
 __global__ void __launch_bounds__(256)
     tridiag_persist_kernel(const float* __restrict__ G, float* xbuf, unsigned* bar, int* err,
                            float* __restrict__ Vh, float* __restrict__ tau,
-                           float* __restrict__ tdiag, float* __restrict__ toff) {
+                           float* __restrict__ tdiag, float* __restrict__ toff, int fenced) {
   constexpr int n = N, CW = 16, NR = N / 16, NV = N / 256, NWG = N / CW;
   const int c0 = blockIdx.x * CW;
   const int tid = threadIdx.x;
@@ -1096,11 +1096,15 @@ __global__ void __launch_bounds__(256)
     } else if (k + 1 >= n) {
       break;
     }
-    // grid barrier (step k): the exchange stores above are complete and
-    // visible (release) before the arrival; reads after it see them (acquire)
+    // grid barrier (step k): the exchange stores above (agent-scope atomic
+    // stores) are complete before the arrival -- every thread waits for its
+    // own (vmcnt 0) -- and the reads after it are agent-scope atomic loads.
+    // fenced != 0 (FRECSYS_TRIDIAG_FENCE=1, A/B) adds device-scope fences,
+    // which write back / invalidate the whole L2 of the XCD each step.
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (tid == 0) {
-      __threadfence();
+      if (fenced) __threadfence();
       atomicAdd(bar, 1u);
       const unsigned target = (unsigned)(k + 1) * NWG;
       unsigned spins = 0;
@@ -1112,7 +1116,7 @@ __global__ void __launch_bounds__(256)
           break;
         }
       }
-      __threadfence();
+      if (fenced) __threadfence();
     }
     __syncthreads();
   }
@@ -1294,12 +1298,14 @@ hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff
     int* err = reinterpret_cast<int*>(work + 4 * (size_t)Dp + 1);
     hipError_t e = hipMemsetAsync(bar, 0, 2 * sizeof(float), s);
     if (e != hipSuccess) return e;
+    const char* fv = getenv("FRECSYS_TRIDIAG_FENCE");
+    const int fenced = fv && atoi(fv) != 0;
     if (Dp == 512)
       hipLaunchKernelGGL(tridiag_persist_kernel<512>, dim3(512 / 16), dim3(256), 0, s, G, xbuf, bar,
-                         err, Vh, tau, tdiag, toff);
+                         err, Vh, tau, tdiag, toff, fenced);
     else
       hipLaunchKernelGGL(tridiag_persist_kernel<1024>, dim3(1024 / 16), dim3(256), 0, s, G, xbuf,
-                         bar, err, Vh, tau, tdiag, toff);
+                         bar, err, Vh, tau, tdiag, toff, fenced);
     return hipGetLastError();
   }
   const int n = Dp;

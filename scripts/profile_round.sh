@@ -6,6 +6,9 @@
 #      summarised into profiles/latest_pmc.json by scripts/pmc_summary.py
 #   3. serialised streams (FRECSYS_DUAL_SERIAL=1): kernel stats + one SQ pass
 #      (MFMA busy, wait/issue stalls) of the headline workload
+#   4. scripts/gather_prof.sh: the MSD item half-step's fabric bytes (marker-
+#      bracketed FETCH / WRITE passes) and the FETCH_SIZE width calibration,
+#      merged into latest_pmc.json (halfstep_item)
 # Usage: profile_round.sh <outdir under gpurun_out> [workloads...]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
@@ -28,4 +31,8 @@ done
 SARGS="--workload ials_ml20m_d256 --extras= --steps 2 --warmup 1 --cpu-seconds 0 --quiet --allow-env"
 FRECSYS_DUAL_SERIAL=1 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/trace_serial -o run --output-format csv -- python3 bench.py $SARGS > $OUT/trace_serial.log 2>&1 || { echo serial trace failed; exit 6; }
 FRECSYS_DUAL_SERIAL=1 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/sq_serial -o run --output-format csv -- python3 bench.py $SARGS > $OUT/sq_serial.log 2>&1 || { echo sq pass failed; exit 7; }
+# the gather on a table past the Infinity Cache (MSD item half-step) + the
+# FETCH_SIZE calibration of the access widths
+./scripts/gather_prof.sh $1/gather ials_msd_d512 item || { echo gather prof failed; exit 8; }
+python3 scripts/pmc_halfstep.py $OUT/gather/fetch/run_counter_collection.csv $OUT/gather/write/run_counter_collection.csv $OUT/gather/probe.json 2.0 $OUT/gather_msd_item.json $OUT/latest_pmc.json > /dev/null || { echo halfstep summary failed; exit 9; }
 echo done
