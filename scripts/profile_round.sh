@@ -13,7 +13,8 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/$1
+NAME=$1
+OUT=gpurun_out/$NAME
 shift
 WL=${*:-ials_ml20m_d256 safer2_ml20m_d256 ials_msd_d512}
 mkdir -p $OUT
@@ -33,6 +34,6 @@ FRECSYS_DUAL_SERIAL=1 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $O
 FRECSYS_DUAL_SERIAL=1 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/sq_serial -o run --output-format csv -- python3 bench.py $SARGS > $OUT/sq_serial.log 2>&1 || { echo sq pass failed; exit 7; }
 # the gather on a table past the Infinity Cache (MSD item half-step) + the
 # FETCH_SIZE calibration of the access widths
-./scripts/gather_prof.sh $1/gather ials_msd_d512 item || { echo gather prof failed; exit 8; }
+./scripts/gather_prof.sh $NAME/gather ials_msd_d512 item || { echo gather prof failed; exit 8; }
 python3 scripts/pmc_halfstep.py $OUT/gather/fetch/run_counter_collection.csv $OUT/gather/write/run_counter_collection.csv $OUT/gather/probe.json 2.0 $OUT/gather_msd_item.json $OUT/latest_pmc.json > /dev/null || { echo halfstep summary failed; exit 9; }
 echo done
