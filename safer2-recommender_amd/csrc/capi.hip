@@ -166,6 +166,17 @@ struct frecsys_ctx {
   uint64_t xrot_gram[2] = {0, 0};   // ... and the basis it was rotated into
   bool dual_used[3] = {false, false, false};  // the side's last solve took history space
   int eager_on = 1;                 // FRECSYS_EAGER=0: no early basis builds (A/B)
+  // Basis kind per side: 0 = tridiagonal (G = Q T Q^T, any mu / lambda per
+  // entity), 1 = Cholesky of the one M = mu*G + lam*I every entity of the
+  // consumer's launch shares (q[] then holds L^-T, tri[][0] its status).
+  // want_*: what the consumer's last history-space solve used (early builds).
+  int basis_mode[2] = {0, 0};
+  float basis_mu[2] = {0.f, 0.f}, basis_lam[2] = {0.f, 0.f};
+  int want_mode[2] = {0, 0};
+  float want_mu[2] = {0.f, 0.f}, want_lam[2] = {0.f, 0.f};
+  int chol_basis_on = 1;            // FRECSYS_CHOL_BASIS=0: always tridiagonal (A/B, tests)
+  float* chol_work = nullptr;
+  size_t cap_chol_work = 0;
   hipStream_t stream5 = nullptr;  // early basis builds: an alias of stream3
   hipEvent_t ev_pre5 = nullptr;
   hipEvent_t ev_eager[2] = {nullptr, nullptr};
@@ -373,7 +384,8 @@ void emb_written(frecsys_ctx* c, int side) { c->emb_ver[side] = ++c->ver_counter
 // Basis of the other side's Gramian, G = Q T Q^T, and the other side
 // rotated into it (X Q): the inputs of the history-space solve.  Rebuilt
 // only when the Gramian (basis) or the rows (rotation) changed since.
-int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
+int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s, int mode = 0,
+                  float mu = 0.f, float lam = 0.f) {
   const int Dp = c->Dp;
   size_t cap = 0;
   if (!c->q[other]) {
@@ -386,7 +398,11 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
     rc = ensure(c, &c->refl[other], &cap, (size_t)Dp * Dp + Dp);
     if (rc) return rc;
   }
-  const bool need_basis = c->basis_gram[other] == 0 || c->basis_gram[other] != c->gram_ver[other];
+  if (mode == 0) mu = lam = 0.f;
+  const bool same_kind = c->basis_mode[other] == mode && c->basis_mu[other] == mu &&
+                         c->basis_lam[other] == lam;
+  const bool need_basis = c->basis_gram[other] == 0 ||
+                          c->basis_gram[other] != c->gram_ver[other] || !same_kind;
   const uint64_t xkey = X == c->emb[other] ? c->emb_ver[other] : 0;
   const bool need_rot = need_basis || xkey == 0 || c->xrot_emb[other] != xkey ||
                         c->xrot_gram[other] != c->gram_ver[other];
@@ -407,6 +423,28 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
     return FRECSYS_OK;
   }
   c->basis_gram[other] = c->gram_ver[other];
+  {  // Cholesky + triangular inverse n^3/3 + n^3/3; Householder reduction 4n^3/3 + Q 4n^3/3
+    const double n = Dp;
+    add_work(c, mode == 1 ? "basis_chol" : "basis_tridiag",
+             mode == 1 ? 2.0 * n * n * n / 3.0 : 8.0 * n * n * n / 3.0, 2.0 * n * n * 4.0, 1);
+  }
+  c->basis_mode[other] = mode;
+  c->basis_mu[other] = mu;
+  c->basis_lam[other] = lam;
+  for (int t = 0; t < 2; ++t)  // bf16-piece images of the forward and back rotations
+    if (!c->qsplit[other][t]) HIP_TRY(c, hipMalloc(&c->qsplit[other][t], basis_split_bytes(Dp)));
+  if (mode == 1) {
+    // q = L^-T: forward X L^-T (image of q), back x' L^-1 (image of q^T)
+    rc = ensure(c, &c->chol_work, &c->cap_chol_work, chol_basis_work_floats(Dp));
+    if (rc) return rc;
+    HIP_TRY(c, launch_chol_basis(c->gram[other], Dp, mu, lam, c->chol_work, c->q[other],
+                                 c->tri[other], s));
+    HIP_TRY(c, launch_split_basis(c->q[other], Dp, 0, c->qsplit[other][0], s));
+    HIP_TRY(c, launch_split_basis(c->q[other], Dp, 1, c->qsplit[other][1], s));
+    HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp,
+                             s));
+    return FRECSYS_OK;
+  }
   float* tau = c->refl[other] + (size_t)Dp * Dp;
   if (wide_dim(Dp)) {
     rc = ensure(c, &c->tri_work, &c->cap_tri_work, wide_tridiag_work_floats(Dp));
@@ -414,8 +452,6 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s) {
   }
   HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp, c->refl[other],
                             tau, s, c->tri_work));
-  for (int t = 0; t < 2; ++t)  // bf16-piece images of Q (forward) and Q^T (back)
-    if (!c->qsplit[other][t]) HIP_TRY(c, hipMalloc(&c->qsplit[other][t], basis_split_bytes(Dp)));
   HIP_TRY(c, launch_form_q(c->refl[other], tau, Dp, c->q[other], s, c->qsplit[other][0],
                            c->qsplit[other][1]));
   HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp, s));
@@ -431,11 +467,13 @@ int maybe_start_eager(frecsys_ctx* c, int g) {
       !c->dual_used[consumer] || c->eager_pending[g])
     return FRECSYS_OK;
   if (c->basis_gram[g] == c->gram_ver[g] && c->xrot_emb[g] == c->emb_ver[g] &&
-      c->xrot_gram[g] == c->gram_ver[g])
+      c->xrot_gram[g] == c->gram_ver[g] && c->basis_mode[g] == c->want_mode[g] &&
+      c->basis_mu[g] == c->want_mu[g] && c->basis_lam[g] == c->want_lam[g])
     return FRECSYS_OK;  // already current
   HIP_TRY(c, hipEventRecord(c->ev_pre5, c->stream));
   HIP_TRY(c, hipStreamWaitEvent(c->stream5, c->ev_pre5, 0));
-  int rc = prepare_basis(c, g, c->emb[g], c->stream5);
+  int rc = prepare_basis(c, g, c->emb[g], c->stream5, c->want_mode[g], c->want_mu[g],
+                         c->want_lam[g]);
   if (rc) return rc;
   HIP_TRY(c, hipEventRecord(c->ev_eager[g], c->stream5));
   c->eager_pending[g] = true;
@@ -766,8 +804,13 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   }
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_HIP, "hipEventCreate failed"));
+  int s3_pri = 0;  // FRECSYS_S3_PRIO=1: the second bucket lane / early builds at high priority
+  if (const char* v = getenv("FRECSYS_S3_PRIO"); v && atoi(v)) {
+    int lo_pri = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo_pri, &s3_pri);
+  }
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, s3_pri) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork3, hipEventDisableTiming) != hipSuccess ||
@@ -786,6 +829,7 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
     return bail(fail(c, FRECSYS_ERR_HIP, "hipEventCreate failed (early builds)"));
   if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
   if (const char* v = getenv("FRECSYS_EAGER")) c->eager_on = atoi(v);
+  if (const char* v = getenv("FRECSYS_CHOL_BASIS")) c->chol_basis_on = atoi(v);
   // d-space / history-space crossover: by flops h = d, but at Dp <= 256 the
   // d-space kernel overtakes the TH = 8 bucket (225 < h <= 256) in time (epoch
   // 15.6 -> 15.1 ms at the ML-20M shape, threshold sweep in DESIGN.md 3.2); at
@@ -860,6 +904,7 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
     if (c->out_rot[s]) (void)hipFree(c->out_rot[s]);
   if (c->dual_table) (void)hipFree(c->dual_table);
   if (c->tri_work) (void)hipFree(c->tri_work);
+  if (c->chol_work) (void)hipFree(c->chol_work);
   if (c->wide_ws) (void)hipFree(c->wide_ws);
   if (c->d_scores) (void)hipFree(c->d_scores);
   if (c->d_rows) (void)hipFree(c->d_rows);
@@ -1398,8 +1443,22 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       // behind them; stream2 waits only for what preceded the fork
       hipStream_t s2 = c->dual_serial ? c->stream : c->stream2;
       if (n_dspace > 0) HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
+      // one M = mu*G + lam*I for every entity (iALS with l2_reg_exp = 0, or
+      // lambda = reg: ials.h:310-315): the Cholesky basis, no tridiagonal
+      // reduction, no per-entity LDL
+      int bmode = 0;
+      float bmu = 0.f, blam = 0.f;
+      if (c->chol_basis_on && c->Dp <= 512 && kind == FRECSYS_KIND_IALS &&
+          (p->lambda_is_reg || p->reg_exp == 0.0f)) {
+        bmode = 1;
+        bmu = p->unobserved_weight;
+        blam = p->reg;
+      }
+      c->want_mode[other] = bmode;
+      c->want_mu[other] = bmu;
+      c->want_lam[other] = blam;
       size_t k = ktimer_begin(c, pre + ".basis", c->stream);
-      rc = prepare_basis(c, other, a.X, c->stream);
+      rc = prepare_basis(c, other, a.X, c->stream, bmode, bmu, blam);
       if (rc) return rc;
       ktimer_end(c, k, c->stream);
       if (n_dspace > 0) {
@@ -1418,6 +1477,8 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       d.Xrot = c->xrot[other];
       d.tdiag = c->tri[other];
       d.toff = c->tri[other] + c->Dp;
+      d.unit_m = bmode;
+      d.basis_status = c->tri[other];
       d.n_other = a.n_other;
       d.reg = a.reg;
       d.reg_exp = a.reg_exp;
@@ -1475,7 +1536,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       d.order = a.order + n_dspace;
       d.n_rows = n_hs;
       d.pos0 = 0;
-      HIP_TRY(c, launch_dual_sweep(d, c->stream));
+      if (!bmode) HIP_TRY(c, launch_dual_sweep(d, c->stream));  // unit table: identity
       ktimer_end(c, k, c->stream);
       {  // h x h system per entity: S = I + Z D^-1 Z^T (h^2 d), its LLT (h^3 / 3),
          // the recurrence and Y^T z (4 h d); rows read twice, the LDL row

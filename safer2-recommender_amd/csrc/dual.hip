@@ -106,6 +106,21 @@ __device__ __forceinline__ void dual_scalars(const DualArgs& a, int64_t e, int64
 __global__ void __launch_bounds__(256) dual_ldl_kernel(DualArgs a) {
   __shared__ float td[kMaxDp], to[kMaxDp];
   const int Dp = a.Dp, tid = threadIdx.x;
+  if (a.unit_m) {
+    // Cholesky basis (spectral.hip chol_basis_kernel): the rows are already
+    // in the basis where M = I, so the table is the unit one; a failed
+    // factorisation of M fails every entity of the launch
+    const int64_t p = (int64_t)blockIdx.x * 256 + tid;
+    if (p >= a.n_rows) return;
+    const int64_t pp = a.pos0 + p;
+    for (int k = 0; k < Dp; ++k) {
+      a.table[blk_t(pp, 0, k, Dp)] = 0.0f;
+      a.table[blk_t(pp, 1, k, Dp)] = 1.0f;
+      a.table[blk_t(pp, 2, k, Dp)] = 1.0f;
+    }
+    if (!(a.basis_status[0] > 0.5f)) atomicMin(a.fail, (unsigned long long)(a.order[p].entity + 1));
+    return;
+  }
   for (int k = tid; k < Dp; k += 256) {
     td[k] = a.tdiag[k];
     to[k] = a.toff[k];

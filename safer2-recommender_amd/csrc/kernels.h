@@ -127,6 +127,10 @@ struct DualArgs {
   const float* Xrot;        // other side rotated into the T basis: X Q, ld Dp
   const float* tdiag;       // [Dp] diagonal of T
   const float* toff;        // [Dp] T(k+1, k)
+  // Cholesky basis (launch_chol_basis: one M for every entity, Xrot = X L^-T):
+  // the LDL table is the unit one and *basis_status = 0 fails the launch
+  int unit_m;
+  const float* basis_status;
   int64_t n_other;
   // position-blocked buffers (64 positions per block, k-major inside a
   // block: every access by consecutive positions is coalesced), position =
@@ -179,6 +183,12 @@ hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hi
 // bf16 (16-B granules in MFMA fragment order).
 size_t basis_split_bytes(int Dp);
 hipError_t launch_split_basis(const float* Q, int Dp, int trans, void* out, hipStream_t s);
+// Cholesky basis of M = mu*G + lam*I (one workgroup): XT = L^-T (Dp x Dp,
+// row-major, upper triangular) with M = L L^T; status[0] = 1, or 0 on a
+// non-positive pivot.  work: chol_basis_work_floats(Dp).  Dp = 64..256, 512.
+size_t chol_basis_work_floats(int Dp);
+hipError_t launch_chol_basis(const float* G, int Dp, float mu, float lam, float* work, float* XT,
+                             float* status, hipStream_t s);
 // Y[row] = X[row] * B with B given by its split image (launch_split_basis),
 // fp32-accurate products on the bf16 matrix cores,
 // for rows r0..r0+n-1, or for the entities rows[0..n) when rows != nullptr

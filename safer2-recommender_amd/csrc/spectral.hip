@@ -19,6 +19,7 @@
 
 #include <type_traits>
 
+#include "chol.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -567,6 +568,149 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ---- Cholesky basis: one M for every entity of the launch ----
+// When every entity of a history-space launch has the same
+// M = mu*G + lam*I (iALS with l2_reg_exp = 0: RegularizationValue,
+// ials.h:310-315, is reg whatever the history; mu = unobserved_weight), the
+// basis need not diagonalise G at all: with M = L L^T, W = X L^-T gives
+// Xt M^-1 Xt^T = W_h W_h^T and x = L^-T (W_h^T z), so dual.hip runs
+// unchanged on W with a unit LDL table (l = 0, D = 1) and the back rotation
+// multiplies by L^-1.  One workgroup of 16 waves:
+//  * right-looking blocked Cholesky over the 32x32 tiles of M in a global
+//    workspace A (L2-resident): wave 0 factors and inverts the diagonal
+//    tile (chol.h diag_factor_inv), the panel L_ip = A_ip L_pp^-T and the
+//    trailing A_ij -= L_ip L_jp^T are f32 MFMA tile products (tile_pqT) over
+//    LDS copies, one tile per wave;
+//  * XT = L^-T by block rows of L: XT_ji = -(sum_{k=j}^{i-1} XT_jk L_ik^T)
+//    L_ii^-T (X = L^-1: L_ii X_ij = -sum_k L_ik X_kj), XT_ii = L_ii^-T.
+// status[0] = 1 when every pivot was positive, else 0 (dual_ldl_kernel turns
+// 0 into the launch's failure flag: the call reruns on the d-space path).
+template <int T>
+__global__ void __launch_bounds__(1024)
+    chol_basis_kernel(const float* __restrict__ G, float mu, float lam, float* __restrict__ A,
+                      float* __restrict__ dinv, float* __restrict__ XT,
+                      float* __restrict__ status) {
+  constexpr int Dp = 32 * T, NW = 16;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* panel = sm;               // [T-1] swizzled tiles: panel p / block row i of L
+  float* D = sm + (T - 1) * 1024;  // L_pp^-1, swizzled
+  float* stg = D + 1024;           // [NW] per-wave staging tile
+  __shared__ int fail;
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid == 0) fail = 0;
+  for (int e4 = tid; e4 < Dp * Dp / 4; e4 += 1024) {  // A = mu*G + lam*I, XT = 0
+    const int r = (4 * e4) / Dp, c = (4 * e4) % Dp;
+    float4 g = reinterpret_cast<const float4*>(G)[e4];
+    g.x = mu * g.x + (r == c ? lam : 0.0f);
+    g.y = mu * g.y + (r == c + 1 ? lam : 0.0f);
+    g.z = mu * g.z + (r == c + 2 ? lam : 0.0f);
+    g.w = mu * g.w + (r == c + 3 ? lam : 0.0f);
+    reinterpret_cast<float4*>(A)[e4] = g;
+    reinterpret_cast<float4*>(XT)[e4] = float4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();
+  // one wave: the 32x32 tile at src (ld Dp) into a swizzled LDS tile
+  auto load_tile = [&](float* dst, const float* src) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e4 = lane + 64 * q, r = e4 >> 3, c = 4 * (e4 & 7);
+      const float4 v = *reinterpret_cast<const float4*>(src + r * Dp + c);
+      dst[sw(r, c)] = v.x;
+      dst[sw(r, c + 1)] = v.y;
+      dst[sw(r, c + 2)] = v.z;
+      dst[sw(r, c + 3)] = v.w;
+    }
+  };
+  for (int p = 0; p < T; ++p) {
+    const int m = T - 1 - p;
+    if (wave == 0) {
+      load_tile(D, A + (32 * p) * Dp + 32 * p);
+      if (!diag_factor_inv(D, lane) && lane == 0) fail = 1;
+      for (int e = lane; e < 1024; e += 64) dinv[p * 1024 + e] = D[e];
+    }
+    __syncthreads();
+    for (int s = wave; s < m; s += NW) {  // L_ip = A_ip L_pp^-T
+      const int i = p + 1 + s;
+      float* slot = panel + s * 1024;
+      load_tile(slot, A + (32 * i) * Dp + 32 * p);
+      const f32x16 u = tile_pqT(slot, D, lo, hi);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int r = acc_row(q, hi);
+        slot[sw(r, lo)] = u[q];
+        A[(32 * i + r) * Dp + 32 * p + lo] = u[q];
+      }
+    }
+    __syncthreads();
+    for (int t = wave; t < m * (m + 1) / 2; t += NW) {  // A_ij -= L_ip L_jp^T
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= t) ++I;
+      const int J = t - I * (I + 1) / 2;
+      float* dst = A + (32 * (p + 1 + I)) * Dp + 32 * (p + 1 + J);
+      float old[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) old[q] = dst[acc_row(q, hi) * Dp + lo];
+      const f32x16 u = tile_pqT(panel + I * 1024, panel + J * 1024, lo, hi);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dst[acc_row(q, hi) * Dp + lo] = old[q] - u[q];
+    }
+    __syncthreads();
+  }
+  for (int i = 0; i < T; ++i) {
+    for (int e = tid; e < i * 1024; e += 1024) {  // block row i of L, tiles k < i
+      const int k = e >> 10, r = (e >> 5) & 31, c = e & 31;
+      panel[k * 1024 + sw(r, c)] = A[(32 * i + r) * Dp + 32 * k + c];
+    }
+    D[tid] = dinv[i * 1024 + tid];
+    __syncthreads();
+    if (wave == NW - 1) {  // XT_ii = L_ii^-T (j < i <= T - 1 < NW - 1 never uses this wave)
+      for (int e = lane; e < 1024; e += 64) {
+        const int r = e >> 5, c = e & 31;
+        XT[(32 * i + c) * Dp + 32 * i + r] = D[sw(r, c)];
+      }
+    }
+    for (int j = wave; j < i; j += NW) {
+      f32x16 acc = f32x16{0.f};
+      for (int k = j; k < i; ++k) {  // C^T = sum_k XT_jk L_ik^T
+        const float* src = XT + (32 * j + lo) * Dp + 32 * k + hi;
+        float pa[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) pa[s] = src[2 * s];
+        const float* Lk = panel + k * 1024;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = mfma32(pa[s], Lk[sw(lo, 2 * s + hi)], acc);
+      }
+      float* st = stg + wave * 1024;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) st[sw(acc_row(q, hi), lo)] = acc[q];
+      const f32x16 u = tile_pqT(st, D, lo, hi);  // XT_ji = -C^T L_ii^-T
+#pragma unroll
+      for (int q = 0; q < 16; ++q) XT[(32 * j + acc_row(q, hi)) * Dp + 32 * i + lo] = -u[q];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) status[0] = fail ? 0.0f : 1.0f;
+}
+
+template <int T>
+hipError_t launch_chol_basis_t(const float* G, float mu, float lam, float* work, float* XT,
+                               float* status, hipStream_t s) {
+  const size_t lds = (size_t)(T + 16) * 1024 * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t err = hipFuncSetAttribute((const void*)chol_basis_kernel<T>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (err != hipSuccess) return err;
+    attr = true;
+  }
+  float* A = work;
+  float* dinv = work + (size_t)32 * T * 32 * T;
+  hipLaunchKernelGGL(chol_basis_kernel<T>, dim3(1), dim3(1024), lds, s, G, mu, lam, A, dinv, XT,
+                     status);
+  return hipGetLastError();
+}
+
 template <int DP>
 hipError_t launch_rotate_t(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
                            const bf16x8* Bs, float* Y, hipStream_t s, int xb,
@@ -608,6 +752,23 @@ hipError_t launch_form_q(const float* Vh, const float* tau, int Dp, float* Q, hi
 }
 
 size_t basis_split_bytes(int Dp) { return (size_t)Dp * Dp * 3 * sizeof(__bf16); }
+
+size_t chol_basis_work_floats(int Dp) { return (size_t)Dp * Dp + (size_t)(Dp / 32) * 1024; }
+
+hipError_t launch_chol_basis(const float* G, int Dp, float mu, float lam, float* work, float* XT,
+                             float* status, hipStream_t s) {
+  switch (Dp) {
+    case 64: return launch_chol_basis_t<2>(G, mu, lam, work, XT, status, s);
+    case 96: return launch_chol_basis_t<3>(G, mu, lam, work, XT, status, s);
+    case 128: return launch_chol_basis_t<4>(G, mu, lam, work, XT, status, s);
+    case 160: return launch_chol_basis_t<5>(G, mu, lam, work, XT, status, s);
+    case 192: return launch_chol_basis_t<6>(G, mu, lam, work, XT, status, s);
+    case 224: return launch_chol_basis_t<7>(G, mu, lam, work, XT, status, s);
+    case 256: return launch_chol_basis_t<8>(G, mu, lam, work, XT, status, s);
+    case 512: return launch_chol_basis_t<16>(G, mu, lam, work, XT, status, s);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 hipError_t launch_split_basis(const float* Q, int Dp, int trans, void* out, hipStream_t s) {
   if (Dp < 64 || Dp % 32 != 0) return hipErrorInvalidValue;

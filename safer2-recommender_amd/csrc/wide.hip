@@ -1126,6 +1126,160 @@ __global__ void __launch_bounds__(256)
     tdiag[0] = __builtin_nanf("");
 }
 
+// The same kernel without the grid barrier: every exchanged value travels
+// with the step that produced it, as one 64-bit word (tag << 32 | bits,
+// tag = base + step + 1, base a per-launch epoch so a previous launch's words
+// never match), stored and polled with agent-scope atomics.  A workgroup
+// starts step k as soon as the values it reads -- p_{k-1} and row k, rows
+// >= k -- carry step k's tag: no arrival counter, no second round trip,
+// and workgroups whose columns are all finished leave.  Ping-pong buffers
+// still suffice: a workgroup can only reach step k+1 (writing buffer k & 1)
+// once every producer has finished step k, whose reads of buffer k & 1 came
+// first.  Same arithmetic and order: bit-identical to the barrier kernel.
+__device__ __forceinline__ void tstore(unsigned long long* p, unsigned tag, float v) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float tpoll(const unsigned long long* p, unsigned tag, int* err) {
+  unsigned spins = 0;
+  while (true) {
+    const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(v >> 32) == tag) return __uint_as_float((unsigned)v);
+    if (++spins > (1u << 20)) {
+      atomicExch(err, 1);
+      return 0.0f;
+    }
+    if ((spins & 255) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return 0.0f;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <int N>
+__global__ void __launch_bounds__(256)
+    tridiag_tagged_kernel(const float* __restrict__ G, unsigned long long* xb, unsigned base,
+                          int* err, float* __restrict__ Vh, float* __restrict__ tau,
+                          float* __restrict__ tdiag, float* __restrict__ toff) {
+  constexpr int n = N, CW = 16, NR = N / 16, NV = N / 256, NWG = N / CW;
+  const int c0 = blockIdx.x * CW;
+  const int tid = threadIdx.x;
+  const int c = c0 + (tid & (CW - 1)), rg = tid >> 4;
+  const bool writer = blockIdx.x == NWG - 1;
+  __shared__ float vp[N], wv[N], vk[N];
+  __shared__ float red[8];
+  __shared__ float pc[16][CW + 1];
+  __shared__ float tsh;
+  float sreg[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) sreg[i] = G[(int64_t)(rg + 16 * i) * n + c];
+  for (int r = tid; r < N; r += 256) vp[r] = 0.0f;
+  if (tid == 0) tsh = 0.0f;
+  __syncthreads();
+  for (int k = 0; k < n; ++k) {
+    if (!(c0 + CW > k + 1 || writer)) return;  // my columns are final (workgroup-uniform)
+    const unsigned long long* pin = xb + (size_t)(k & 1) * 2 * N;
+    unsigned long long* pout = xb + (size_t)((k + 1) & 1) * 2 * N;
+    const unsigned tin = base + (unsigned)k, tout = base + (unsigned)k + 1;
+    const float tp = tsh;
+    float pir[NV], akr[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int r = tid + 256 * j;
+      pir[j] = (k > 0 && r >= k) ? tpoll(pin + r, tin, err) : 0.0f;
+      akr[j] = r >= k ? (k == 0 ? G[r] : tpoll(pin + N + r, tin, err)) : 0.0f;
+    }
+    float d = 0.0f;
+    if (tp != 0.0f) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) d += pir[j] * vp[tid + 256 * j];
+    }
+    d = block_sum(d, red);
+    const float K = -0.5f * tp * d;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int r = tid + 256 * j;
+      wv[r] = (tp != 0.0f && r >= k) ? pir[j] + K * vp[r] : 0.0f;
+    }
+    __syncthreads();
+    const float vpk = vp[k], wk = wv[k];
+    float xn = 0.0f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int r = tid + 256 * j;
+      if (r >= k) {
+        const float ck = akr[j] - vpk * wv[r] - wk * vp[r];
+        vk[r] = ck;
+        if (r >= k + 2) xn += ck * ck;
+      }
+    }
+    xn = block_sum(xn, red);
+    const float dkk = vk[k];
+    float beta = 0.0f, tk = 0.0f, scal = 0.0f;
+    if (k + 1 < n) {
+      const float alpha = vk[k + 1];
+      if (xn == 0.0f) {
+        beta = alpha;
+        tk = 0.0f;
+      } else {
+        beta = -copysignf(sqrtf(alpha * alpha + xn), alpha);
+        tk = (beta - alpha) / beta;
+        scal = 1.0f / (alpha - beta);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int r = tid + 256 * j;
+      float v = 0.0f;
+      if (r == k + 1) v = 1.0f;
+      else if (r >= k + 2) v = tk != 0.0f ? vk[r] * scal : 0.0f;
+      vk[r] = v;
+    }
+    __syncthreads();
+    if (writer) {
+      if (tid == 0) {
+        tdiag[k] = dkk;
+        toff[k] = k + 1 < n ? beta : 0.0f;
+        tau[k] = tk;
+      }
+      if (k + 1 < n)
+        for (int r = k + 1 + tid; r < n; r += 256) Vh[(int64_t)k * n + r] = vk[r];
+    }
+    if (k + 1 >= n) break;
+    const bool col_live = c >= k + 1 && c < n;
+    float pacc = 0.0f;
+    if (col_live) {
+      const float vpc = vp[c], wc = wv[c];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const int r = rg + 16 * i;
+        if (r >= k + 1) {
+          const float v = sreg[i] - vp[r] * wc - wv[r] * vpc;
+          sreg[i] = v;
+          pacc += v * vk[r];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NR; ++i)
+        if (rg + 16 * i == k + 1) tstore(pout + N + c, tout, sreg[i]);  // row k+1, my column
+    }
+    pc[rg][tid & (CW - 1)] = pacc;
+    __syncthreads();
+    if (tid < CW) {
+      const int cc = c0 + tid;
+      float sum = 0.0f;
+#pragma unroll
+      for (int g2 = 0; g2 < 16; ++g2) sum += pc[g2][tid];
+      if (cc >= k + 1 && cc < n) tstore(pout + cc, tout, tk * sum);
+    }
+    for (int r = tid; r < N; r += 256) vp[r] = vk[r];
+    if (tid == 0) tsh = tk;
+    __syncthreads();
+  }
+  if (writer && tid == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    tdiag[0] = __builtin_nanf("");
+}
+
 // User loss at wide Dp: one wave per user, Dp/32 lanes per history row
 // (8 float4 each), 64*32/Dp rows in flight; u^T G u from the rotate_kernel
 // partials (one per 128-column block) summed in column-block order.
@@ -1300,6 +1454,23 @@ hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff
     if (e != hipSuccess) return e;
     const char* fv = getenv("FRECSYS_TRIDIAG_FENCE");
     const int fenced = fv && atoi(fv) != 0;
+    // default: the tagged exchange (2.48 vs 2.96 ms at 512, 7.40 vs 8.51 at
+    // 1024 alone, bit-identical; scripts/micro/tridiag_wide_bench.cpp);
+    // FRECSYS_TRIDIAG_TAGGED=0: the barrier kernel (A/B)
+    const char* tv = getenv("FRECSYS_TRIDIAG_TAGGED");
+    const bool tagged = !tv || atoi(tv) != 0;
+    if (tagged) {  // tagged words [2][2][Dp] after the counters; cleared per launch
+      unsigned long long* xb = reinterpret_cast<unsigned long long*>(work + 8 * (size_t)Dp);
+      e = hipMemsetAsync(xb, 0, 4 * (size_t)Dp * sizeof(unsigned long long), s);
+      if (e != hipSuccess) return e;
+      if (Dp == 512)
+        hipLaunchKernelGGL(tridiag_tagged_kernel<512>, dim3(512 / 16), dim3(256), 0, s, G, xb, 0u,
+                           err, Vh, tau, tdiag, toff);
+      else
+        hipLaunchKernelGGL(tridiag_tagged_kernel<1024>, dim3(1024 / 16), dim3(256), 0, s, G, xb,
+                           0u, err, Vh, tau, tdiag, toff);
+      return hipGetLastError();
+    }
     if (Dp == 512)
       hipLaunchKernelGGL(tridiag_persist_kernel<512>, dim3(512 / 16), dim3(256), 0, s, G, xbuf, bar,
                          err, Vh, tau, tdiag, toff, fenced);

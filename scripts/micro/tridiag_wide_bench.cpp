@@ -37,10 +37,11 @@ int main(int argc, char** argv) {
     hipEventCreate(&a);
     hipEventCreate(&b);
     std::vector<float> ref;
-    for (int variant = 0; variant < 3; ++variant) {
+    for (int variant = 0; variant < 4; ++variant) {
       const int steps = variant == 2;
       setenv("FRECSYS_TRIDIAG_STEPS", steps ? "1" : "0", 1);
       setenv("FRECSYS_TRIDIAG_FENCE", variant == 1 ? "1" : "0", 1);
+      setenv("FRECSYS_TRIDIAG_TAGGED", variant == 3 ? "1" : "0", 1);  // default on in the library
       float best = 1e9f;
       for (int it = 0; it < 5; ++it) {
         hipEventRecord(a);
@@ -55,7 +56,7 @@ int main(int argc, char** argv) {
       hipMemcpy(o.data(), dd, 4 * n, hipMemcpyDeviceToHost);
       hipMemcpy(o.data() + n, de, 4 * n, hipMemcpyDeviceToHost);
       if (variant == 0) ref = o;
-      const char* name[3] = {"persistent", "persistent+fences", "step launches"};
+      const char* name[4] = {"persistent", "persistent+fences", "step launches", "tagged"};
       printf("n=%d %s: %.3f ms (%.2f us/step) %s\n", n, name[variant], best, best * 1e3 / n,
              memcmp(o.data(), ref.data(), 8 * n) == 0 ? "bit-identical" : "DIFFERS");
     }

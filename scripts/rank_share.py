@@ -7,8 +7,8 @@ rotation of the whole other side, loss of its own users -- and skips only the
 RCCL exchange.  max over ranks of that time + the modelled exchange is the
 N-GPU epoch; the gap to T(1)/N is the replicated work.
 
-Usage: rank_share.py [workload] [steps] [N rank]   (workload as bench.py; iALS
-only; with N rank: that one rank only, e.g. under rocprofv3 --kernel-trace for
+Usage: rank_share.py [workload] [steps] [N [rank]]   (workload as bench.py; iALS
+only; with N: every rank of that N only; with N rank: that one rank only, e.g. under rocprofv3 --kernel-trace for
 scripts/timeline_summary.py)
 Prints one JSON line per (N, rank) and a summary line.
 """
@@ -36,13 +36,14 @@ def main():
     wl = sys.argv[1] if len(sys.argv) > 1 else "ials_ml20m_d256"
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     only = (int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else None
+    only_n = int(sys.argv[3]) if len(sys.argv) == 4 else None
     spec = WORKLOADS[wl]
     assert spec["model"] == "ials", "iALS workloads only"
     f = spec["flags"]
     up, uc, ip, ic = synthetic(SHAPES[spec["shape"]])
     nu, ni = len(up) - 1, len(ip) - 1
     summary = {}
-    for N in ((only[0],) if only else (1, 2, 4, 8)):
+    for N in ((only[0],) if only else ((only_n,) if only_n else (1, 2, 4, 8))):
         per_rank = []
         for r in ((only[1],) if only else range(N)):
             ctx = fh.Context(spec["dim"], nu, ni)
@@ -79,6 +80,9 @@ def main():
             ctx.close()
         summary[N] = {"max_ms": max(per_rank), "mean_ms": float(np.mean(per_rank))}
     if only:
+        return
+    if only_n:
+        print(json.dumps({"summary": summary}), flush=True)
         return
     t1 = summary[1]["max_ms"]
     for N, s in summary.items():

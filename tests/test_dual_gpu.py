@@ -61,23 +61,31 @@ def _both_paths(monkeypatch, make, max_h=None):
 
 @pytest.mark.parametrize("dim", [64, 96, 128, 256])
 @pytest.mark.parametrize("max_h", [256, 64])
-def test_ials_dual_vs_dspace_vs_oracle(monkeypatch, quirk_data, dim, max_h):
+@pytest.mark.parametrize("reg_exp", [1.0, 0.0])
+def test_ials_dual_vs_dspace_vs_oracle(monkeypatch, quirk_data, dim, max_h, reg_exp):
+    """iALS with the default l2_reg_exp = 1 (lambda per user: the tridiagonal
+    basis) and with l2_reg_exp = 0 (one M = w G + reg I for every user: the
+    Cholesky basis)."""
     nu, ni, up, uc, ip, ic = quirk_data
     reg, w = 0.003, 0.1
     V0 = _spread_embeddings(ni, dim, 8)
+    basis = "chol" if reg_exp == 0.0 else "tridiag"
 
     def run():
         ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
         ctx.set_embeddings(fh.SIDE_ITEM, V0)
         ctx.gramian(fh.SIDE_ITEM)
         ctx.timing_reset()
-        ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, reg, w)
+        ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, reg, w, reg_exp=reg_exp)
         hs = ctx.timing("solve_user.hspace")[1]
+        if hs:
+            assert ctx.work("basis_chol")[2] == (basis == "chol")
+            assert ctx.work("basis_tridiag")[2] == (basis == "tridiag")
         return ctx.get_embeddings(fh.SIDE_USER), U, hs
 
     (Ud, U, hs0), (Uh, _, hs1) = _both_paths(monkeypatch, run, max_h)
     assert hs0 == 0 and hs1 == 1  # the split really happened
-    Uo, rc = O.step(up, uc, V0, O.gramian(V0), 0, reg, w, out=U.copy())
+    Uo, rc = O.step(up, uc, V0, O.gramian(V0), 0, reg, w, reg_exp=reg_exp, out=U.copy())
     assert rc == 0
     assert rel_rows(Ud, Uo).max() < TOL_ROW
     assert rel_rows(Uh, Uo).max() < TOL_ROW
@@ -85,6 +93,37 @@ def test_ials_dual_vs_dspace_vs_oracle(monkeypatch, quirk_data, dim, max_h):
     h = np.diff(up)
     long = h > max_h
     np.testing.assert_array_equal(Uh[long], Ud[long])  # same kernel for the long ones
+
+
+@pytest.mark.parametrize("dim", [128, 256, 512])
+@pytest.mark.parametrize("reg,w", [(0.003, 0.1), (1e-5, 1.0)])
+def test_chol_basis_conditioning(monkeypatch, quirk_data, dim, reg, w):
+    """iALS with l2_reg_exp = 0: the Cholesky basis against the tridiagonal
+    one (FRECSYS_CHOL_BASIS=0) and the oracle on a wide spectrum, including an ill-conditioned M (reg 1e-5, w 1: cond(M)
+    ~ 1e8): the explicit L^-T may not lose more than the tridiagonal LDL
+    chains do."""
+    nu, ni, up, uc, ip, ic = quirk_data
+    V0 = _spread_embeddings(ni, dim, 12)
+    monkeypatch.setenv("FRECSYS_DUAL", "1")
+    monkeypatch.setenv("FRECSYS_DUAL_MAX_H", "256")
+    outs = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("FRECSYS_CHOL_BASIS", on)
+        ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+        ctx.set_embeddings(fh.SIDE_ITEM, V0)
+        ctx.gramian(fh.SIDE_ITEM)
+        ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, reg, w, reg_exp=0.0)
+        assert ctx.work("basis_chol")[2] == (on == "1")
+        outs.append(ctx.get_embeddings(fh.SIDE_USER))
+        ctx.close()
+    Uo, rc = O.step(up, uc, V0, O.gramian(V0), 0, reg, w, reg_exp=0.0, out=U.copy())
+    assert rc == 0
+    h = np.diff(up)
+    hs = (h > 0) & (h <= 256)
+    e_chol = rel_rows(outs[0][hs], Uo[hs]).max()
+    e_tri = rel_rows(outs[1][hs], Uo[hs]).max()
+    print(f"dim {dim} reg {reg} w {w}: chol {e_chol:.2e} tridiag {e_tri:.2e}")
+    assert e_chol < max(TOL_ROW, 3.0 * e_tri), (e_chol, e_tri)
 
 
 @pytest.mark.parametrize("dim", [64, 128, 256])
