@@ -711,10 +711,155 @@ hipError_t launch_chol_basis_t(const float* G, float mu, float lam, float* work,
   return hipGetLastError();
 }
 
+// rotate_kernel with RT row tiles per wave (64 RT rows per workgroup) and
+// the X rows loaded P k-steps ahead (a register ring): at the MSD shape the
+// one-step-ahead loads of rotate_kernel left it waiting on HBM (MFMA busy
+// ~0.27), and each B fragment now feeds RT tiles.  Same products in the same
+// k order per output element as rotate_kernel: bit-identical.
+template <int DP, int RT, int P>
+__global__ void __launch_bounds__(256)
+    rotate_rt_kernel(const float* __restrict__ X, const QueueRec* __restrict__ rows, int64_t r0,
+                     int64_t n, const bf16x8* __restrict__ Bs, float* __restrict__ Y,
+                     int x_blocked, int ncb) {
+  constexpr int NCT = DP / 32, NS = DP / 16;
+  static_assert(NS % P == 0, "k steps a multiple of the prefetch depth");
+  constexpr int CW = (DP % 128 == 0) ? 2 : 1;
+  constexpr int CB = 2 * CW;
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t bid = blockIdx.x, sx = bid >> 3;
+  const int cbk = (int)(sx % ncb);
+  const int64_t rblk = (sx / ncb) * 8 + (bid & 7);
+  const int64_t base = rblk * 64 * RT;
+  if (base >= n) return;
+  const int R = wave & 1, cg = wave >> 1;
+  const int C0 = cbk * CB + cg * CW;
+  int64_t pos[RT];
+  bool pv[RT];
+  const float* xr[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    pos[t] = base + 32 * (R * RT + t) + lo;
+    pv[t] = pos[t] < n;
+    xr[t] = X + (x_blocked ? 0 : (r0 + (pv[t] ? pos[t] : base)) * DP);
+  }
+  f32x16 acc[RT][CW];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int j = 0; j < CW; ++j) acc[t][j] = f32x16{0.f};
+  auto load_a = [&](int s, float (&v)[RT][8]) __attribute__((always_inline)) {
+    const int k0 = 16 * s + 8 * hi;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      if (x_blocked) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[t][j] = pv[t] ? X[blk_v(pos[t], k0 + j, DP)] : 0.0f;
+      } else {
+        const float4 a = *reinterpret_cast<const float4*>(xr[t] + k0);
+        const float4 b = *reinterpret_cast<const float4*>(xr[t] + k0 + 4);
+        v[t][0] = a.x, v[t][1] = a.y, v[t][2] = a.z, v[t][3] = a.w;
+        v[t][4] = b.x, v[t][5] = b.y, v[t][6] = b.z, v[t][7] = b.w;
+      }
+    }
+  };
+  float va[P][RT][8];  // X ring: step s in slot s % P
+#pragma unroll
+  for (int u = 0; u < P - 1; ++u) load_a(u, va[u]);
+  bf16x8 bn[CW][3];
+  auto load_b = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const int C = C0 + j < NCT ? C0 + j : NCT - 1;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bn[j][p] = Bs[((int64_t)(s * NCT + C) * 3 + p) * 64 + lane];
+    }
+  };
+  load_b(0);
+  for (int s0 = 0; s0 < NS; s0 += P) {
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      const int s = s0 + u;
+      bf16x8 bf[CW][3];
+#pragma unroll
+      for (int j = 0; j < CW; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bf[j][p] = bn[j][p];
+      if (s + P - 1 < NS) load_a(s + P - 1, va[(u + P - 1) % P]);
+      if (s + 1 < NS) load_b(s + 1);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = pv[t] ? va[u][t][j] : 0.0f;
+        bf16x8 af[3];
+        split3x8(v, af);
+#pragma unroll
+        for (int j = 0; j < CW; ++j)
+          if (C0 + j < NCT) acc[t][j] = mfma_x6(af, bf[j], acc[t][j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const int C = C0 + j;
+      if (C >= NCT) continue;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t p = base + 32 * (R * RT + t) + acc_row(q, hi);
+        if (p < n) {
+          const int64_t id = rows ? (int64_t)rows[p].entity : r0 + p;
+          Y[id * DP + 32 * C + lo] = acc[t][j][q];
+        }
+      }
+    }
+}
+
+// FRECSYS_ROT_RT (A/B): 0 = rotate_kernel, 1 / 2 = rotate_rt_kernel row tiles
+// per wave.  Default 2: 1.95 vs 2.20 ms for the 471,355 x 512 rotation, 0.138
+// vs 0.141 ms for 116,677 x 256, bit-identical (scripts/micro/rotate_bench.cpp)
+int rotate_rt() {
+  const char* v = getenv("FRECSYS_ROT_RT");
+  return v ? atoi(v) : 2;
+}
+int rotate_p() {  // 4 measured no better than 2 (scripts/micro/rotate_bench.cpp)
+  const char* v = getenv("FRECSYS_ROT_P");
+  return v ? atoi(v) : 2;
+}
+
+template <int DP, int RT>
+void launch_rotate_rtp(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
+                       const bf16x8* Bs, float* Y, hipStream_t s, int xb, int ncb, int p) {
+  const int64_t units = (n + 64 * RT - 1) / (64 * RT);
+  const unsigned grid = (unsigned)(((units + 7) / 8) * 8 * ncb);
+  constexpr int NS = DP / 16;
+  if constexpr (NS % 4 == 0) {
+    if (p == 4) {
+      hipLaunchKernelGGL((rotate_rt_kernel<DP, RT, 4>), dim3(grid), dim3(256), 0, s, X, rows, r0,
+                         n, Bs, Y, xb, ncb);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((rotate_rt_kernel<DP, RT, 2>), dim3(grid), dim3(256), 0, s, X, rows, r0, n,
+                     Bs, Y, xb, ncb);
+}
+
 template <int DP>
 hipError_t launch_rotate_t(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
                            const bf16x8* Bs, float* Y, hipStream_t s, int xb,
                            float* qpart = nullptr) {
+  constexpr int CBc = (DP % 128 == 0) ? 4 : 2;
+  const int ncbc = (DP / 32 + CBc - 1) / CBc;
+  const int rt = qpart ? 0 : rotate_rt();
+  if (rt == 1 || rt == 2) {
+    if (rt == 1)
+      launch_rotate_rtp<DP, 1>(X, rows, r0, n, Bs, Y, s, xb, ncbc, rotate_p());
+    else
+      launch_rotate_rtp<DP, 2>(X, rows, r0, n, Bs, Y, s, xb, ncbc, rotate_p());
+    return hipGetLastError();
+  }
   constexpr int CB = (DP % 128 == 0) ? 4 : 2;
   const int ncb = (DP / 32 + CB - 1) / CB;
   const int64_t units = (n + 63) / 64;
