@@ -57,7 +57,12 @@ namespace {
 
 constexpr int WB = 128;    // block-pair edge
 constexpr int WR = 16;     // rows per staged chunk
-constexpr int kWideMaxBlocks = 256;  // leaves of a Gramian (kernels.h GramPlan)
+constexpr int kWideMaxBlocks = 256;  // row blocks of the wide SYRK launches
+// Leaves of a wide Gramian (kernels.h GramPlan): 768 rather than 256, so that
+// a rank's two of the 16 groups at N = 8 still launch ~100 leaves x the block
+// pairs (the 1,842-row leaves of 256 took 376 us for the MSD user Gramian on
+// 96 workgroups); the leaf structure depends on n only (partition-independent)
+constexpr int kWideGramLeaves = 768;
 
 __device__ __forceinline__ void pair_of(int pidx, int& BI, int& BJ) {
   BI = 0;
@@ -1362,7 +1367,11 @@ size_t wide_slab_floats(int Dp) {
   return (size_t)T * (T + 1) / 2 * 1024 + 2 * (size_t)Dp;
 }
 
-int64_t wide_rows_per_leaf(int64_t n) { return wide_rows_per_block(n); }
+int64_t wide_rows_per_leaf(int64_t n) {
+  int64_t rpl = (n + kWideGramLeaves - 1) / kWideGramLeaves;
+  if (rpl < 256) rpl = 256;
+  return (rpl + WR - 1) / WR * WR;
+}
 
 hipError_t launch_wide_gram_leaves(int Dp, const GramArgs& g, hipStream_t s) {
   if (!wide_dim(Dp)) return hipErrorInvalidValue;
