@@ -446,9 +446,19 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s, int 
     return FRECSYS_OK;
   }
   float* tau = c->refl[other] + (size_t)Dp * Dp;
-  if (wide_dim(Dp)) {
-    rc = ensure(c, &c->tri_work, &c->cap_tri_work, wide_tridiag_work_floats(Dp));
+  const bool qpipe = tridiag_forms_q(Dp);
+  if (wide_dim(Dp) || qpipe) {
+    rc = ensure(c, &c->tri_work, &c->cap_tri_work, tridiag_work_floats(Dp));
     if (rc) return rc;
+  }
+  if (qpipe) {
+    // Q rows and their split images formed inside the reduction's launch
+    HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp,
+                              c->refl[other], tau, s, c->tri_work, c->q[other],
+                              c->qsplit[other][0], c->qsplit[other][1]));
+    HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp,
+                             s));
+    return FRECSYS_OK;
   }
   HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp, c->refl[other],
                             tau, s, c->tri_work));

@@ -167,4 +167,110 @@ __device__ __forceinline__ float cvar_upper(int kind, float g, float w, float om
   return w * g;
 }
 
+
+// ---- tagged words: a value and the step that produced it in one 64-bit
+// word, stored and polled with agent-scope atomics (no fence, no barrier
+// counter: a reader takes the word once its tag matches).  Cross-workgroup
+// exchange of the persistent tridiagonalisation (wide.hip) and of the
+// reflectors it publishes to the Q-row workers (qrows_worker below).
+__device__ __forceinline__ void tstore(unsigned long long* p, unsigned tag, float v) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// Bounded wait (~2^24 polls): on timeout *err (if given) is set and 0 / NaN
+// (nan_on_timeout) returned, so a caller never spins forever.
+__device__ __forceinline__ float tpoll(const unsigned long long* p, unsigned tag, int* err,
+                                       bool nan_on_timeout = false) {
+  unsigned spins = 0;
+  while (true) {
+    const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(v >> 32) == tag) return __uint_as_float((unsigned)v);
+    if (++spins > (1u << 24)) {
+      if (err) atomicExch(err, 1);
+      return nan_on_timeout ? __builtin_nanf("") : 0.0f;
+    }
+    if (err && (spins & 255) == 0 &&
+        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      return nan_on_timeout ? __builtin_nanf("") : 0.0f;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Rows of Q = H_0 H_1 ... H_{nsteps-1} by forward accumulation, consuming the
+// reflectors as a tridiagonalisation publishes them: row r of Q starts as
+// e_r and takes q_r <- q_r - tau_k (q_r . v_k) v_k^T per step (rows are
+// independent).  One workgroup of NT threads owns rows 32*wid .. +31, NT/32
+// threads per row, columns c = cs + (NT/32) j in registers.  Reflector k:
+// vt[k * n + r] (r > k, tag k+1; entries r <= k are zero), tau_k: tt[k]
+// (tag k+1).  vsh: LDS [2][NMAX], tau2: LDS [2] (double-buffered, one
+// barrier per step).  A timed-out poll leaves NaN in the rows (the history-
+// space pivots then fail and the call reruns in d-space).  At the end the
+// rows go to Q (row-major); the workgroup then reads its 32 rows back (its
+// own stores, visible after the barrier) into its granules of the split
+// images of Q and Q^T that the rotations read (split_basis_kernel's layout;
+// n a multiple of 32): row groups 2 wid, 2 wid + 1 of Q's image, column
+// block wid of Q^T's.  (Staging them in LDS instead would size every
+// workgroup of the reduction's launch for it: 64 / 128 KB at 512 / 1024.)
+template <int NMAX, int NT>
+__device__ __forceinline__ void qrows_worker(int wid, int n, int nsteps,
+                                             const unsigned long long* vt,
+                                             const unsigned long long* tt, float* Q,
+                                             bf16x8* img_q, bf16x8* img_qt, float* vsh,
+                                             float* tau2) {
+  constexpr int TPR = NT / 32, NC = NMAX / TPR;
+  const int tid = threadIdx.x, rr = tid / TPR, cs = tid % TPR;
+  const int row = 32 * wid + rr;
+  float q[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) q[j] = (cs + TPR * j == row) ? 1.0f : 0.0f;
+  for (int k = 0; k < nsteps; ++k) {
+    float* v = vsh + (k & 1) * NMAX;
+    for (int r = tid; r < NMAX; r += NT)
+      v[r] = (r > k && r < n) ? tpoll(vt + (size_t)k * n + r, k + 1, nullptr, true) : 0.0f;
+    if (tid == 0) tau2[k & 1] = tpoll(tt + k, k + 1, nullptr, true);
+    __syncthreads();
+    const float tau = tau2[k & 1];
+    if (tau != 0.0f) {  // workgroup-uniform
+      float d = 0.0f;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) d += q[j] * v[cs + TPR * j];
+#pragma unroll
+      for (int o = 1; o < TPR; o <<= 1) d += __shfl_xor(d, o);
+      d *= tau;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) q[j] -= d * v[cs + TPR * j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int c = cs + TPR * j;
+    if (row < n && c < n) Q[(size_t)row * n + c] = q[j];
+  }
+  __syncthreads();
+  if (!img_q || 32 * wid >= n) return;
+  const float* qb = Q + (size_t)32 * wid * n;  // my 32 rows
+  const int nct = n / 32, ns = n / 16;
+  for (int g = tid; g < 2 * nct * 64; g += NT) {  // Q: rows 16 s + 8 hi .. +7 of column 32 C + lo
+    const int lane = g & 63, lo = lane & 31, hi = lane >> 5;
+    const int sc = g >> 6, C = sc % nct, s = 2 * wid + sc / nct;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = qb[(size_t)(16 * (s - 2 * wid) + 8 * hi + j) * n + 32 * C + lo];
+    bf16x8 f[3];
+    split3x8(x, f);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) img_q[((size_t)(s * nct + C) * 3 + p) * 64 + lane] = f[p];
+  }
+  for (int g = tid; g < ns * 64; g += NT) {  // Q^T: B[k][col] = Q[col][k], col = 32 wid + lo
+    const int lane = g & 63, lo = lane & 31, hi = lane >> 5;
+    const int s = g >> 6;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = qb[(size_t)lo * n + 16 * s + 8 * hi + j];
+    bf16x8 f[3];
+    split3x8(x, f);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) img_qt[((size_t)(s * nct + wid) * 3 + p) * 64 + lane] = f[p];
+  }
+}
 }  // namespace frecsys_hip

@@ -171,9 +171,15 @@ hipError_t launch_dual_sweep(const DualArgs& a, hipStream_t s);
 hipError_t launch_dual(int tiles, const DualArgs& a, hipStream_t s);
 // Householder tridiagonalisation G = Q T Q^T of a Dp x Dp symmetric matrix
 // (one workgroup): T's diagonal / subdiagonal, the reflectors (row k of Vh,
-// entries k+1..Dp-1) and their tau.
+// entries k+1..Dp-1) and their tau.  With Q (only when tridiag_forms_q(Dp)):
+// Q itself too, row-major, formed by workgroups of the same launch as the
+// reflectors are published (work: tridiag_work_floats(Dp)), and with
+// img_q / img_qt the split images of Q and Q^T (launch_split_basis's layout).
 hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
-                          float* tau, hipStream_t s, float* work = nullptr);
+                          float* tau, hipStream_t s, float* work = nullptr, float* Q = nullptr,
+                          void* img_q = nullptr, void* img_qt = nullptr);
+bool tridiag_forms_q(int Dp);
+size_t tridiag_work_floats(int Dp);
 // Q = H_0 H_1 ... H_{Dp-3} from the reflectors, row-major Dp x Dp; with
 // img_q / img_qt also the split images of Q and Q^T (launch_split_basis's
 // layout, basis_split_bytes each; Dp a multiple of 32).
@@ -267,8 +273,10 @@ hipError_t launch_wide_gram_final(int Dp, const float* gslabs, int64_t ngroup, f
 hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batch,
                              hipStream_t s);
 size_t wide_tridiag_work_floats(int Dp);
+bool wide_tridiag_tagged();
 hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
-                               float* tau, float* work, hipStream_t s);
+                               float* tau, float* work, hipStream_t s, float* Q = nullptr,
+                               void* img_q = nullptr, void* img_qt = nullptr);
 size_t wide_quad_floats(int Dp, int64_t rows);
 hipError_t launch_wide_user_loss(int Dp, const LossArgs& a, hipStream_t s);
 hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s);

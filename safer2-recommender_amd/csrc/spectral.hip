@@ -106,13 +106,22 @@ __device__ unsigned long long g_tri_prof[16][8];  // [wave][phase]
 // never waited on inside the loop.  K = (tau/2) v.p is formed by every wave
 // from the published p.  Step k only needs the trailing block
 // [k+1:, k+1:], so waves whose 32 rows are all <= k skip its arithmetic.
+// With Q != nullptr, workgroups 1 .. n/32 form the rows of Q while the
+// reduction runs (common.h qrows_worker): at the start of step k the first n
+// threads store v_k (its LDS copy, tau-masked) and tau_k as tagged words
+// (vt, tt), so no form-Q launch follows.
 __global__ void __launch_bounds__(512)
     tridiag_kernel(const float* __restrict__ G, int n, float* tdiag, float* toff, float* Vh,
-                   float* tau_out) {
+                   float* tau_out, float* Q, bf16x8* img_q, bf16x8* img_qt,
+                   unsigned long long* vt, unsigned long long* tt) {
   typedef float f2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 operands
   __shared__ __attribute__((aligned(16))) float vs[2][256];
   __shared__ __attribute__((aligned(16))) float ps[256];
   __shared__ float tsh[2];
+  if (blockIdx.x > 0) {  // Q-row worker (reflectors k = 0 .. n-3)
+    qrows_worker<256, 512>(blockIdx.x - 1, n, n - 2, vt, tt, Q, img_q, img_qt, &vs[0][0], tsh);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int rb = 4 * wave + (lane >> 4);  // row block (8 rows)
@@ -191,6 +200,10 @@ __global__ void __launch_bounds__(512)
     TRI_PROF_MARK(0)
     const float tau = tsh[k & 1];
     const float* v = vs[k & 1];
+    if (Q) {  // reflector k for the Q-row workers, from its LDS copy (published at step k)
+      if (tid > k && tid < n) tstore(vt + (size_t)k * n + tid, (unsigned)k + 1, v[tid]);
+      if (tid == 0) tstore(tt + k, (unsigned)k + 1, tau);
+    }
     const bool active = 32 * wave + 31 >= k + 1;  // wave-uniform: rows > k present
     const bool owner = wave == ((k + 1) >> 5);    // forms reflector k+1 inside its update
     f2 vc[8];
@@ -871,11 +884,36 @@ hipError_t launch_rotate_t(const float* X, const QueueRec* rows, int64_t r0, int
 
 }  // namespace
 
+bool qpipe_on() {  // FRECSYS_QPIPE=0: form Q by form_q_kernel after the reduction (A/B)
+  const char* v = getenv("FRECSYS_QPIPE");
+  return !v || atoi(v) != 0;
+}
+
+bool tridiag_forms_q(int Dp) {
+  if (!qpipe_on() || Dp < 64 || Dp % 32) return false;
+  return wide_dim(Dp) ? wide_tridiag_tagged() : Dp <= 256;
+}
+
+size_t tridiag_work_floats(int Dp) {
+  return wide_dim(Dp) ? wide_tridiag_work_floats(Dp) : (size_t)2 * Dp * Dp + 2 * (size_t)Dp;
+}
+
 hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
-                          float* tau, hipStream_t s, float* work) {
-  if (wide_dim(Dp)) return launch_wide_tridiag(G, Dp, tdiag, toff, Vh, tau, work, s);
+                          float* tau, hipStream_t s, float* work, float* Q, void* img_q,
+                          void* img_qt) {
+  if (Q && (!tridiag_forms_q(Dp) || !work)) return hipErrorInvalidValue;
+  if ((img_q != nullptr) != (img_qt != nullptr) || (img_q && !Q)) return hipErrorInvalidValue;
+  if (wide_dim(Dp)) return launch_wide_tridiag(G, Dp, tdiag, toff, Vh, tau, work, s, Q, img_q, img_qt);
   if (Dp < 4 || Dp > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(512), 0, s, G, Dp, tdiag, toff, Vh, tau);
+  unsigned long long* vt = Q ? reinterpret_cast<unsigned long long*>(work) : nullptr;
+  unsigned long long* tt = Q ? vt + (size_t)Dp * Dp : nullptr;
+  if (Q) {
+    hipError_t e = hipMemsetAsync(vt, 0, ((size_t)Dp * Dp + Dp) * sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+  }
+  const unsigned grid = 1 + (Q ? (unsigned)(Dp / 32) : 0u);
+  hipLaunchKernelGGL(tridiag_kernel, dim3(grid), dim3(512), 0, s, G, Dp, tdiag, toff, Vh, tau, Q,
+                     reinterpret_cast<bf16x8*>(img_q), reinterpret_cast<bf16x8*>(img_qt), vt, tt);
   return hipGetLastError();
 }
 

@@ -1141,39 +1141,33 @@ __global__ void __launch_bounds__(256)
 // still suffice: a workgroup can only reach step k+1 (writing buffer k & 1)
 // once every producer has finished step k, whose reads of buffer k & 1 came
 // first.  Same arithmetic and order: bit-identical to the barrier kernel.
-__device__ __forceinline__ void tstore(unsigned long long* p, unsigned tag, float v) {
-  __hip_atomic_store(p, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float tpoll(const unsigned long long* p, unsigned tag, int* err) {
-  unsigned spins = 0;
-  while (true) {
-    const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((unsigned)(v >> 32) == tag) return __uint_as_float((unsigned)v);
-    if (++spins > (1u << 20)) {
-      atomicExch(err, 1);
-      return 0.0f;
-    }
-    if ((spins & 255) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      return 0.0f;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
+// With Q != nullptr the grid carries N/32 more workgroups that form the
+// rows of Q as the reflectors are published (common.h qrows_worker; the
+// writer stores v_k and tau_k as tagged words into vt / tt), so no form-Q
+// launch follows the reduction.
 template <int N>
 __global__ void __launch_bounds__(256)
     tridiag_tagged_kernel(const float* __restrict__ G, unsigned long long* xb, unsigned base,
                           int* err, float* __restrict__ Vh, float* __restrict__ tau,
-                          float* __restrict__ tdiag, float* __restrict__ toff) {
+                          float* __restrict__ tdiag, float* __restrict__ toff, float* Q,
+                          bf16x8* img_q, bf16x8* img_qt, unsigned long long* vt,
+                          unsigned long long* tt) {
   constexpr int n = N, CW = 16, NR = N / 16, NV = N / 256, NWG = N / CW;
+  __shared__ float lbuf[3 * N];
+  float* vp = lbuf;
+  float* wv = lbuf + N;
+  float* vk = lbuf + 2 * N;
+  __shared__ float red[8];
+  __shared__ float pc[16][CW + 1];
+  __shared__ float tsh;
+  if (blockIdx.x >= NWG) {  // Q-row worker (reflectors k = 0 .. n-2)
+    qrows_worker<N, 256>(blockIdx.x - NWG, n, n - 1, vt, tt, Q, img_q, img_qt, lbuf, red);
+    return;
+  }
   const int c0 = blockIdx.x * CW;
   const int tid = threadIdx.x;
   const int c = c0 + (tid & (CW - 1)), rg = tid >> 4;
   const bool writer = blockIdx.x == NWG - 1;
-  __shared__ float vp[N], wv[N], vk[N];
-  __shared__ float red[8];
-  __shared__ float pc[16][CW + 1];
-  __shared__ float tsh;
   float sreg[NR];
 #pragma unroll
   for (int i = 0; i < NR; ++i) sreg[i] = G[(int64_t)(rg + 16 * i) * n + c];
@@ -1246,9 +1240,13 @@ __global__ void __launch_bounds__(256)
         tdiag[k] = dkk;
         toff[k] = k + 1 < n ? beta : 0.0f;
         tau[k] = tk;
+        if (Q && k + 1 < n) tstore(tt + k, (unsigned)k + 1, tk);
       }
       if (k + 1 < n)
-        for (int r = k + 1 + tid; r < n; r += 256) Vh[(int64_t)k * n + r] = vk[r];
+        for (int r = k + 1 + tid; r < n; r += 256) {
+          Vh[(int64_t)k * n + r] = vk[r];
+          if (Q) tstore(vt + (size_t)k * n + r, (unsigned)k + 1, vk[r]);
+        }
     }
     if (k + 1 >= n) break;
     const bool col_live = c >= k + 1 && c < n;
@@ -1445,7 +1443,18 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
 
 // persistent kernel: exchange [2][2][Dp] + barrier counter + error flag; the
 // step kernels (FRECSYS_TRIDIAG_STEPS=1, A/B): two Dp x Dp copies + two p
-size_t wide_tridiag_work_floats(int Dp) { return (size_t)2 * Dp * Dp + 2 * (size_t)Dp; }
+// (+ the tagged reflector words of the Q-row workers: 2 Dp^2 + 2 Dp floats more)
+size_t wide_tridiag_work_floats(int Dp) { return (size_t)4 * Dp * Dp + 32 * (size_t)Dp; }
+
+// default: the tagged exchange (2.48 vs 2.96 ms at 512, 7.40 vs 8.51 at
+// 1024 alone, bit-identical; scripts/micro/tridiag_wide_bench.cpp);
+// FRECSYS_TRIDIAG_TAGGED=0: the barrier kernel, FRECSYS_TRIDIAG_STEPS=1 one
+// launch per step (A/B)
+bool wide_tridiag_tagged() {
+  const char* tv = getenv("FRECSYS_TRIDIAG_TAGGED");
+  const char* sv = getenv("FRECSYS_TRIDIAG_STEPS");
+  return (!tv || atoi(tv) != 0) && !(sv && atoi(sv) != 0);
+}
 
 bool tridiag_steps() {
   const char* v = getenv("FRECSYS_TRIDIAG_STEPS");
@@ -1453,7 +1462,8 @@ bool tridiag_steps() {
 }
 
 hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
-                               float* tau, float* work, hipStream_t s) {
+                               float* tau, float* work, hipStream_t s, float* Q, void* img_q,
+                               void* img_qt) {
   if (!wide_dim(Dp) || !work) return hipErrorInvalidValue;
   if (!tridiag_steps()) {
     float* xbuf = work;                                     // [2][2][Dp]
@@ -1463,21 +1473,24 @@ hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff
     if (e != hipSuccess) return e;
     const char* fv = getenv("FRECSYS_TRIDIAG_FENCE");
     const int fenced = fv && atoi(fv) != 0;
-    // default: the tagged exchange (2.48 vs 2.96 ms at 512, 7.40 vs 8.51 at
-    // 1024 alone, bit-identical; scripts/micro/tridiag_wide_bench.cpp);
-    // FRECSYS_TRIDIAG_TAGGED=0: the barrier kernel (A/B)
-    const char* tv = getenv("FRECSYS_TRIDIAG_TAGGED");
-    const bool tagged = !tv || atoi(tv) != 0;
+    const bool tagged = wide_tridiag_tagged();
     if (tagged) {  // tagged words [2][2][Dp] after the counters; cleared per launch
       unsigned long long* xb = reinterpret_cast<unsigned long long*>(work + 8 * (size_t)Dp);
-      e = hipMemsetAsync(xb, 0, 4 * (size_t)Dp * sizeof(unsigned long long), s);
+      // with Q: the reflectors as tagged words vt [Dp][Dp], tt [Dp], cleared too
+      unsigned long long* vt = xb + 4 * (size_t)Dp;
+      unsigned long long* tt = vt + (size_t)Dp * Dp;
+      const size_t words = 4 * (size_t)Dp + (Q ? (size_t)Dp * Dp + Dp : 0);
+      e = hipMemsetAsync(xb, 0, words * sizeof(unsigned long long), s);
       if (e != hipSuccess) return e;
+      const unsigned grid = (unsigned)(Dp / 16 + (Q ? Dp / 32 : 0));
+      bf16x8* iq = reinterpret_cast<bf16x8*>(img_q);
+      bf16x8* iqt = reinterpret_cast<bf16x8*>(img_qt);
       if (Dp == 512)
-        hipLaunchKernelGGL(tridiag_tagged_kernel<512>, dim3(512 / 16), dim3(256), 0, s, G, xb, 0u,
-                           err, Vh, tau, tdiag, toff);
+        hipLaunchKernelGGL(tridiag_tagged_kernel<512>, dim3(grid), dim3(256), 0, s, G, xb, 0u, err,
+                           Vh, tau, tdiag, toff, Q, iq, iqt, vt, tt);
       else
-        hipLaunchKernelGGL(tridiag_tagged_kernel<1024>, dim3(1024 / 16), dim3(256), 0, s, G, xb,
-                           0u, err, Vh, tau, tdiag, toff);
+        hipLaunchKernelGGL(tridiag_tagged_kernel<1024>, dim3(grid), dim3(256), 0, s, G, xb, 0u,
+                           err, Vh, tau, tdiag, toff, Q, iq, iqt, vt, tt);
       return hipGetLastError();
     }
     if (Dp == 512)

@@ -21,7 +21,7 @@ mkdir -p $OUT
 timeout -k 10 420 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; exit 1; }
 echo "bench ok"
 for w in $WL; do
-  ARGS="--workload $w --extras= --steps 3 --warmup 1 --cpu-seconds 0 --quiet"
+  ARGS="--workload $w --extras= --steps 10 --warmup 1 --cpu-seconds 0 --quiet"
   timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/trace_$w -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace_$w.log 2>&1 || { echo trace $w failed; exit 2; }
   PARGS="--workload $w --extras= --steps 1 --warmup 1 --cpu-seconds 0 --quiet"
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch_$w -o run --output-format csv -- python3 bench.py $PARGS > $OUT/fetch_$w.log 2>&1 || { echo fetch $w failed; exit 3; }
