@@ -352,7 +352,8 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
     K = steps
     d = spec["dim"]
     Dp = fh.padded_dim(d)
-    names = ["solve_user", "solve_item", "gramian", "user_loss", "allgather", "gram_exchange"]
+    names = ["solve_user", "solve_item", "gramian", "user_loss", "user_loss.gather", "allgather",
+             "gram_exchange"]
     names += [f"{s}.{p}" for s in ("solve_user", "solve_item")
               for p in ("dspace", "split", "basis", "hspace", "rotate")]
     timers = {k: ctx.timing(k) for k in names}
@@ -364,7 +365,11 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
     si_ms = timers["solve_item"][0] / max(K, 1)
     gb = gather_bytes(up, ulo, uhi, d, d) + gather_bytes(ip, ilo, ihi, d, d)
     g_gbs = gb / ((su_ms + si_ms) * 1e-3) / 1e9 if su_ms + si_ms > 0 else 0.0
-    loss_ms = timers["user_loss"][0] / max(timers["user_loss"][1], 1)
+    # the gather kernel's own time (library event pair around it), the
+    # kernel the loss_gather roofline prices; the pass (u^T G u + gather)
+    # when the library has no separate timer (Dp <= 16)
+    lg = timers["user_loss.gather"] if timers["user_loss.gather"][1] else timers["user_loss"]
+    loss_ms = lg[0] / max(lg[1], 1)
     lw = ctx.work("user_loss")
     lb = lw[1] / max(lw[3], 1)  # algorithmic bytes per ComputeUserLoss pass (library-accounted)
     l_gbs = lb / (loss_ms * 1e-3) / 1e9 if loss_ms > 0 else 0.0

@@ -1651,9 +1651,21 @@ int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, fl
   a.half = half;
   a.out = c->d_loss;
   {
+    // user_loss: both kernels; user_loss.gather: the gather kernel alone (its
+    // own rate for the loss_gather roofline)
+    frecsys_ctx::Pending g{"user_loss.gather", pool_event(c), pool_event(c)};
+    a.ev_gather = c->Dp > 16 ? g.a : nullptr;
     ScopedTimer t(c, "user_loss");
     HIP_TRY(c, launch_user_loss(c->Dp, a, c->stream));
+    if (a.ev_gather) {
+      (void)hipEventRecord(g.b, c->stream);
+      c->pending.push_back(g);
+    } else {
+      c->event_pool.push_back(g.a);
+      c->event_pool.push_back(g.b);
+    }
     t.stop();
+    flush_ktimers(c);
   }
   if (side == 0) {  // gather of the item rows + u^T G u: SURVEY 8(d) bytes with a 1-float output
     const std::vector<int64_t>& rp = c->host_rp[0];

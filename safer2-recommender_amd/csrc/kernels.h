@@ -108,6 +108,7 @@ struct LossArgs {
   float* quad;           // [rows of side] scratch: u^T G u (Dp >= 32)
   void* gsplit;          // Dp = 512 / 1024: scratch for G's split image (basis_split_bytes)
   int raw;               // 1: out[e] = sum_j (x_j . u - 1)^2 only (train stats)
+  hipEvent_t ev_gather;  // recorded right before the gather kernel (timing), or nullptr
 };
 
 

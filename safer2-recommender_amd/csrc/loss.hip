@@ -218,6 +218,7 @@ hipError_t launch2(const LossArgs& a, hipStream_t s) {
   const unsigned nq = (unsigned)((a.n_rows + 63) / 64);
   if (!a.raw) hipLaunchKernelGGL(quad_kernel<NCT>, dim3(nq), dim3(256), 0, s, a);
   const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
+  if (a.ev_gather) (void)hipEventRecord(a.ev_gather, s);
   hipLaunchKernelGGL(loss_gather_kernel<Dp>, dim3(nb), dim3(256), 0, s, a);
   return hipGetLastError();
 }

@@ -831,7 +831,9 @@ __global__ void __launch_bounds__(256)
 }
 
 // FRECSYS_ROT_RT (A/B): 0 = rotate_kernel, 1 / 2 = rotate_rt_kernel row tiles
-// per wave.  Default 2: 1.95 vs 2.20 ms for the 471,355 x 512 rotation, 0.138
+// per wave.  (An LDS-staged GEMM form -- X block split once per workgroup,
+// B's image copied to LDS, 128 x 128 blocks, two stages -- measured 2.97 ms,
+// slower: one workgroup per CU did not hide the loads.)  Default 2: 1.95 vs 2.20 ms for the 471,355 x 512 rotation, 0.138
 // vs 0.141 ms for 116,677 x 256, bit-identical (scripts/micro/rotate_bench.cpp)
 int rotate_rt() {
   const char* v = getenv("FRECSYS_ROT_RT");

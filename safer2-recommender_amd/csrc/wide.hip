@@ -1530,6 +1530,7 @@ hipError_t launch_wide_user_loss(int Dp, const LossArgs& a, hipStream_t s) {
     if (e != hipSuccess) return e;
   }
   const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
+  if (a.ev_gather) (void)hipEventRecord(a.ev_gather, s);
   if (Dp == 512)
     hipLaunchKernelGGL(loss_gather_wide_kernel<512>, dim3(nb), dim3(256), 0, s, a);
   else
