@@ -33,7 +33,8 @@ int main() {
   hipEventCreate(&b);
   for (int it = 0; it < 3; ++it) {
     hipEventRecord(a);
-    hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(TRI_THREADS), 0, 0, dG, n, dd, de, dV, dt);
+    hipLaunchKernelGGL(tridiag_kernel, dim3(1), dim3(TRI_THREADS), 0, 0, dG, n, dd, de, dV, dt,
+                       nullptr, nullptr, nullptr, nullptr, nullptr);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms;
@@ -56,11 +57,10 @@ int main() {
 // host-side launchers of spectral.hip reference wide.hip; stubs for this harness
 namespace frecsys_hip {
 bool wide_dim(int) { return false; }
-hipError_t launch_wide_tridiag(const float*, int, float*, float*, float*, float*, float*, hipStream_t) {
+hipError_t launch_wide_tridiag(const float*, int, float*, float*, float*, float*, float*, hipStream_t,
+                               float*, void*, void*) {
   return hipErrorInvalidValue;
 }
-hipError_t launch_wide_rot(const float*, const QueueRec*, int64_t, int64_t, const float*, int, float*, int,
-                           hipStream_t, int) {
-  return hipErrorInvalidValue;
-}
+bool wide_tridiag_tagged() { return false; }
+size_t wide_tridiag_work_floats(int) { return 0; }
 }  // namespace frecsys_hip
