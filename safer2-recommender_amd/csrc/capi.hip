@@ -1631,12 +1631,23 @@ int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, fl
     HIP_TRY(c, hipMemsetAsync(c->d_loss, 0, sizeof(float) * std::max<size_t>(rows, 1), c->stream));
   int64_t lo, hi;
   shard(c, side, &lo, &hi);
+  // Dp = 64..256: u^T G u by the rotation kernel (column-block partials) unless
+  // FRECSYS_QUAD_ROT=0 (quad_kernel, f32 MFMA; A/B)
+  static const bool quad_rot = [] {
+    const char* v = getenv("FRECSYS_QUAD_ROT");
+    return !v || atoi(v) != 0;
+  }();
+  const bool qr = !wide_dim(c->Dp) && c->Dp >= 64 && c->Dp % 32 == 0 && quad_rot;
   rc = ensure(c, &c->d_quad, &c->cap_quad,
-              std::max<size_t>(wide_dim(c->Dp) ? wide_quad_floats(c->Dp, hi - lo) : rows, 1));
+              std::max<size_t>(wide_dim(c->Dp) ? wide_quad_floats(c->Dp, hi - lo)
+                               : qr ? (size_t)rotate_quad_parts(c->Dp) * (size_t)(hi - lo)
+                                    : rows,
+                               1));
   if (rc) return rc;
   LossArgs a{};
   a.quad = c->d_quad;
-  if (wide_dim(c->Dp)) {
+  a.quad_parts = qr ? rotate_quad_parts(c->Dp) : 0;
+  if (wide_dim(c->Dp) || qr) {
     if (!c->gsplit) HIP_TRY(c, hipMalloc(&c->gsplit, basis_split_bytes(c->Dp)));
     a.gsplit = c->gsplit;
   }

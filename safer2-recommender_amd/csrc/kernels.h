@@ -105,7 +105,9 @@ struct LossArgs {
   float beta;
   int half;
   float* out;            // [rows of side]
-  float* quad;           // [rows of side] scratch: u^T G u (Dp >= 32)
+  float* quad;           // [rows of side] scratch: u^T G u (Dp >= 32); with quad_parts > 0
+                         // [quad_parts][n_rows] partial sums by launch row (rotate_quad)
+  int quad_parts;
   void* gsplit;          // Dp = 512 / 1024: scratch for G's split image (basis_split_bytes)
   int raw;               // 1: out[e] = sum_j (x_j . u - 1)^2 only (train stats)
   hipEvent_t ev_gather;  // recorded right before the gather kernel (timing), or nullptr
@@ -207,6 +209,8 @@ hipError_t launch_rotate(const float* X, const QueueRec* rows, int64_t r0, int64
 // (X B)[r] .* X[r] for rows r0 .. r0+n-1 (u^T G u partials, B = G).
 hipError_t launch_rotate_quad(const float* X, int64_t r0, int64_t n, const void* bsplit,
                               float* qpart, int Dp, hipStream_t s);
+// Column blocks (partial sums per row) launch_rotate_quad writes at Dp.
+int rotate_quad_parts(int Dp);
 
 __host__ __device__ inline int64_t blk_v(int64_t p, int k, int Dp) {
   return ((p >> 6) * Dp + k) * 64 + (p & 63);

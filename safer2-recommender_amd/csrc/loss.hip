@@ -207,7 +207,14 @@ __global__ void __launch_bounds__(256) loss_gather_kernel(LossArgs a) {
     if (lane == 0) a.out[e] = sq;
     return;
   }
-  float loss = sq / (float)h + a.beta * a.quad[e];
+  float qv;
+  if (a.quad_parts > 0) {  // u^T G u from the rotation kernel's column-block partials
+    qv = 0.0f;
+    for (int b = 0; b < a.quad_parts; ++b) qv += a.quad[(int64_t)b * a.n_rows + idx];
+  } else {
+    qv = a.quad[e];
+  }
+  float loss = sq / (float)h + a.beta * qv;
   if (a.half) loss = (float)((double)loss / 2.0);
   if (lane == 0) a.out[e] = loss;
 }
@@ -216,7 +223,17 @@ template <int NCT>
 hipError_t launch2(const LossArgs& a, hipStream_t s) {
   constexpr int Dp = 32 * NCT;
   const unsigned nq = (unsigned)((a.n_rows + 63) / 64);
-  if (!a.raw) hipLaunchKernelGGL(quad_kernel<NCT>, dim3(nq), dim3(256), 0, s, a);
+  if (!a.raw && a.quad_parts > 0) {
+    // u^T G u as (U G) .* U on the bf16 matrix cores (fp32-accurate split
+    // products; spectral.hip rotate_kernel with the row-dot epilogue): 4x
+    // the rate of quad_kernel's f32 MFMA at Dp = 256
+    hipError_t e = launch_split_basis(a.G, Dp, 0, a.gsplit, s);
+    if (e != hipSuccess) return e;
+    e = launch_rotate_quad(a.U, a.row_lo, a.n_rows, a.gsplit, a.quad, Dp, s);
+    if (e != hipSuccess) return e;
+  } else if (!a.raw) {
+    hipLaunchKernelGGL(quad_kernel<NCT>, dim3(nq), dim3(256), 0, s, a);
+  }
   const unsigned nb = (unsigned)((a.n_rows + 3) / 4);
   if (a.ev_gather) (void)hipEventRecord(a.ev_gather, s);
   hipLaunchKernelGGL(loss_gather_kernel<Dp>, dim3(nb), dim3(256), 0, s, a);

@@ -985,9 +985,23 @@ hipError_t launch_rotate_quad(const float* X, int64_t r0, int64_t n, const void*
                               float* qpart, int Dp, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const bf16x8* B = reinterpret_cast<const bf16x8*>(bsplit);
-  if (Dp == 512) return launch_rotate_t<512>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
-  if (Dp == 1024) return launch_rotate_t<1024>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
-  return hipErrorInvalidValue;
+  switch (Dp) {
+    case 64: return launch_rotate_t<64>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+    case 96: return launch_rotate_t<96>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+    case 128: return launch_rotate_t<128>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+    case 160: return launch_rotate_t<160>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+    case 192: return launch_rotate_t<192>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+    case 224: return launch_rotate_t<224>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+    case 256: return launch_rotate_t<256>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+    case 512: return launch_rotate_t<512>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+    case 1024: return launch_rotate_t<1024>(X, nullptr, r0, n, B, nullptr, s, 0, qpart);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int rotate_quad_parts(int Dp) {
+  const int cb = (Dp % 128 == 0) ? 4 : 2;  // rotate_kernel's column tiles per workgroup
+  return (Dp / 32 + cb - 1) / cb;
 }
 
 }  // namespace frecsys_hip

@@ -4,7 +4,7 @@
 set -o pipefail
 OUT=gpurun_out/$1
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_dual_gpu.py tests/test_eager_gpu.py tests/test_parity_gpu.py > $OUT/pytest.log 2>&1 || { echo pytest failed; tail -20 $OUT/pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_dual_gpu.py tests/test_eager_gpu.py tests/test_parity_gpu.py tests/test_stats_gpu.py tests/test_models_gpu.py tests/test_sharded_gpu.py > $OUT/pytest.log 2>&1 || { echo pytest failed; tail -20 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 for i in 1 2; do
   timeout -k 10 200 python bench.py --steps 20 --warmup 5 --extras= --cpu-seconds 0 > $OUT/bench_$i.json 2> $OUT/bench_$i.err || { echo bench failed; exit 2; }
