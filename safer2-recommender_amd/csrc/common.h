@@ -84,11 +84,17 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+#ifdef FRECSYS_CHEAP_SPLIT  // timing ablation only (wrong numbers): the split's VALU cost
+  h = (__bf16)x;
+  m = (__bf16)0.0f;
+  l = (__bf16)0.0f;
+#else
   h = (__bf16)x;
   float r = x - (float)h;
   m = (__bf16)r;
   r -= (float)m;
   l = (__bf16)r;
+#endif
 }
 
 __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
