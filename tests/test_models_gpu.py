@@ -81,7 +81,7 @@ def ml1m_csr(ml1m):
 
 
 @pytest.mark.parametrize("case", sorted(CASES))
-@pytest.mark.parametrize("dim", [8, 32, 64, 128, 256])
+@pytest.mark.parametrize("dim", [8, 32, 64, 128, 256, 512])
 def test_train_trajectory_matches_oracle(tmp_path, ml1m_csr, case, dim):
     model = case.split("_epan")[0].split("_snr")[0]
     oid, reg, w, alpha, bw, eta, epan, snr = CASES[case]
