@@ -44,13 +44,23 @@ typedef __attribute__((address_space(3))) float lds_float;
 // read: no divergent loads; the asm keeps the select below after the loads
 // instead of turning it into per-element branches).  G = 8 cuts the waits
 // 8x but holds 8 addresses; G = 1 for the register-capped callers.
-template <int G>
+// Element (r, c) of a diagonal tile: the XOR swizzle sw(r, c) (LDP = 0), or
+// rows padded to LDP floats (LDP = 36: constant offsets from one base per
+// lane -- no per-element address registers -- and conflict-free row and
+// column access alike; solve_rr.hip).
+template <int LDP>
+__device__ __forceinline__ int tix(int r, int c) {
+  if constexpr (LDP == 0) return sw(r, c);
+  return r * LDP + c;
+}
+
+template <int G, int LDP = 0>
 __device__ __forceinline__ void load_factor_rows(const lds_float* tile, int r, bool fl,
                                                  float (&a)[32]) {
   if constexpr (G == 1) {
 #pragma unroll
     for (int c = 0; c < 32; ++c) {
-      float t = tile[sw(r, c)];
+      float t = tile[tix<LDP>(r, c)];
       asm volatile("" : "+v"(t));
       a[c] = fl ? t : (c == r ? 1.0f : 0.0f);
     }
@@ -59,7 +69,7 @@ __device__ __forceinline__ void load_factor_rows(const lds_float* tile, int r, b
 #pragma unroll
   for (int c0 = 0; c0 < 32; c0 += G) {
 #pragma unroll
-    for (int c = c0; c < c0 + G; ++c) a[c] = tile[sw(r, c)];
+    for (int c = c0; c < c0 + G; ++c) a[c] = tile[tix<LDP>(r, c)];
 #pragma unroll
     for (int c = c0; c < c0 + G; ++c) asm volatile("" : "+v"(a[c]));
   }
@@ -117,12 +127,13 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
 // in registers by then), and columns 16..31 by the recurrence over
 // m in [16, k) only.  256 v_readlane + 256 FMAs of the serial chain become
 // MFMAs.
-__device__ __noinline__ bool diag_factor_inv_blk(lds_float* tile, int lane) {
+template <int LDP = 0>
+__device__ __forceinline__ bool diag_factor_inv_blk_inl(lds_float* tile, int lane) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   const int r = lane & 31;
   const bool fl = lane < 32;
   float a[32];
-  load_factor_rows<8>(tile, r, fl, a);
+  load_factor_rows<8, LDP>(tile, r, fl, a);
   // pivot test without a vector compare per column: piv > 0 and not NaN
   // <=> its bits as an int lie in (0, 0x7f800000]
   int pmin = 0x7fffffff, pmax = 0;
@@ -191,13 +202,19 @@ __device__ __noinline__ bool diag_factor_inv_blk(lds_float* tile, int lane) {
     // (zero inputs times finite factors): stored as they are
 #pragma unroll
     for (int k = 0; k < 32; ++k)
-      if (!fl) tile[sw(k, j)] = a[k];
+      if (!fl) tile[tix<LDP>(k, j)] = a[k];
   } else {
 #pragma unroll
     for (int k = 0; k < 32; ++k)
-      if (!fl) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
+      if (!fl) tile[tix<LDP>(k, j)] = (k >= j) ? a[k] : 0.0f;
   }
   return ok;
+}
+// As a call: callers with few live registers (the tiled kernels); a caller
+// holding its matrix in registers (solve_rr.hip) inlines the body instead,
+// since a call clobbers half of the VGPRs and the live tiles would spill.
+__device__ __noinline__ bool diag_factor_inv_blk(lds_float* tile, int lane) {
+  return diag_factor_inv_blk_inl<0>(tile, lane);
 }
 
 // BLK = true for kernels with a register budget above ~150 VGPRs (the

@@ -301,5 +301,9 @@ bool syrk_split_bf16();
 // (rows * Dp >= 2^32), or FRECSYS_GATHER64=1 forces them (tests: the two
 // widths are bit-identical).
 bool gather_off64(int64_t rows, int Dp);
+// Register-resident d-space solve at Dp = 256 (solve_rr.hip): two entities
+// per CU; the solve kinds only; opt-in with FRECSYS_RR=1.
+bool solve_rr_enabled(int Dp, int kind);
+hipError_t launch_solve_rr(const SolveArgs& a, hipStream_t s);
 
 }  // namespace frecsys_hip
