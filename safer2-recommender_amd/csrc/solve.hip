@@ -36,6 +36,17 @@
 #include "common.h"
 #include "kernels.h"
 
+// Super-block tile ownership of the split-bf16 SYRK at Dp = 256 (kSbPat):
+// 2 in the split (PARTIAL) and the solve kernels, 1 (default) in the split
+// kernel only, 0 nowhere (tile t to wave t % 8).  All three are bit-identical
+// (scripts/sb_ab_cmd.sh).  Measured (ML-20M d = 256, serialised): split
+// kernel 1.059 vs 1.086 ms/epoch; in the solve kernel the five ownership
+// copies of the SYRK loop spill beside the Cholesky's registers (2.72 vs 2.21
+// ms), so it keeps t % 8 there.
+#ifndef FRECSYS_SYRK_SB
+#define FRECSYS_SYRK_SB 1
+#endif
+
 namespace frecsys_hip {
 
 namespace {
@@ -85,6 +96,39 @@ __device__ __forceinline__ int bf_gran(int p, int g, int hh, int c) {
   return ((p * 2 + g) * 2 + hh) * Dp + c;
 }
 
+// Tile ownership of the split-bf16 SYRK at T = 8 ("super-blocks"): each
+// wave reads the operand fragments of (at most) four column blocks X[0..3]
+// per k step and reuses each for two or more of its tiles -- 12 granule
+// reads per k step instead of 6 per tile (~2.5x less LDS fragment traffic).
+// Waves 0..5 own the six off-diagonal 2x2 super-blocks of the 8x8 tile grid
+// (block rows X0, X1 x block columns X2, X3), waves 6 and 7 diagonal tiles;
+// the sub-diagonal and diagonal tiles left over go where their fragments
+// are already loaded.  Tiles per wave 5,5,5,5,4,4,4,4: waves w and w+4
+// (one SIMD) hold 9 between them, as tile t -> wave t % 8 did.
+//   pattern 0: SB + (X1, X0)  waves 0, 1, 3      pattern 1: SB   waves 4, 5
+//   pattern 2: SB + (X0, X0)  wave 2             pattern 3: (X0,X0) (X1,X0) (X1,X1) (X2,X2)  wave 6
+//   pattern 4: (X0,X0) (X1,X1) (X2,X2) (X3,X3)   wave 7
+// with SB = (X0,X2) (X0,X3) (X1,X2) (X1,X3); slot m = tile (X[pa[m]], X[pb[m]]).
+struct SbPat {
+  int n, pa[5], pb[5];
+};
+__device__ constexpr SbPat kSbPat[5] = {
+    {5, {0, 0, 1, 1, 1}, {2, 3, 2, 3, 0}},
+    {4, {0, 0, 1, 1, 0}, {2, 3, 2, 3, 0}},
+    {5, {0, 0, 1, 1, 0}, {2, 3, 2, 3, 0}},
+    {4, {0, 1, 1, 2, 0}, {0, 0, 1, 2, 0}},
+    {4, {0, 1, 2, 3, 0}, {0, 1, 2, 3, 0}},
+};
+__device__ __forceinline__ int sb_pattern(int wave) {
+  constexpr int pat[8] = {0, 0, 2, 0, 1, 1, 3, 4};
+  return pat[wave];
+}
+__device__ __forceinline__ int sb_block(int wave, int x) {
+  constexpr int blk[8][4] = {{2, 3, 0, 1}, {4, 5, 0, 1}, {4, 5, 2, 3}, {6, 7, 0, 1},
+                             {6, 7, 2, 3}, {6, 7, 4, 5}, {0, 1, 2, 2}, {3, 5, 6, 7}};
+  return blk[wave][x];
+}
+
 // Virtual history position k -> offset within the entity's CSR row: k < h
 // are the real rows; with the tail quirk rows h .. h+extra-1 re-read the
 // positions [h-128, h-r) (safer2.h:200-204).
@@ -103,7 +147,10 @@ template <int T, bool PARTIAL, bool BF, bool OFF64 = false>
 __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     solve_tiled_kernel(SolveArgs a) {
   using C = TiledCfg<T, BF>;
-  constexpr int Dp = C::Dp, NT = C::NT, NW = C::NW, NTHR = C::NTHR, MT = C::MT;
+  // SB: super-block tile ownership (sb_tile) for the split-bf16 SYRK at T = 8
+  constexpr bool SB = BF && T == 8 && (FRECSYS_SYRK_SB >= 2 || (PARTIAL && FRECSYS_SYRK_SB >= 1));
+  constexpr int Dp = C::Dp, NT = C::NT, NW = C::NW, NTHR = C::NTHR;
+  constexpr int MT = C::MT;
   constexpr int R = C::R, NQ = C::NQ, NSLOT = C::NSLOT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* tiles = smem;
@@ -367,11 +414,18 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
   bool valid[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
-    const int t = wave + m * NW;
-    valid[m] = t < NT;
-    int I = 0;
-    while ((I + 1) * (I + 2) / 2 <= t) ++I;
-    const int J = t - I * (I + 1) / 2;
+    int I = 0, J = 0;
+    if constexpr (SB) {
+      const SbPat& pt = kSbPat[sb_pattern(wave)];
+      valid[m] = m < pt.n;
+      I = sb_block(wave, pt.pa[m]);
+      J = sb_block(wave, pt.pb[m]);
+    } else {
+      const int t = wave + m * NW;
+      valid[m] = t < NT;
+      while ((I + 1) * (I + 2) / 2 <= t) ++I;
+      J = t - I * (I + 1) / 2;
+    }
     aoff[m] = 32 * I + lo;
     boff[m] = 32 * J + lo;
     acc[m] = f32x16{0.f};
@@ -383,6 +437,11 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
       }
     }
   }
+  int sbx[4] = {0, 0, 0, 0};  // SB: the wave's four column blocks
+  if constexpr (SB) {
+#pragma unroll
+    for (int x = 0; x < 4; ++x) sbx[x] = sb_block(wave, x);
+  }
   // split entity: add its slabs in slab order (deterministic)
   float bacc = 0.0f;
   const size_t slab_floats = (size_t)NT * 1024 + Dp;
@@ -391,13 +450,61 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       if (valid[m]) {
-        const int t = wave + m * NW;
+        const int t = tidx((aoff[m] - lo) >> 5, (boff[m] - lo) >> 5);
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[m][q] += sl[t * 1024 + q * 64 + lane];
       }
     }
     if (tid < Dp) bacc += sl[NT * 1024 + tid];
   }
+  // The tiles leave the registers right after the SYRK loop (inside each
+  // ownership pattern's copy of it, so the accumulators of the copies never
+  // merge): PARTIAL -> the slab (raw accumulator layout), else -> A in the
+  // swizzled LDS tiles (aliasing the then-dead stage; the loop's last
+  // barrier ordered every stage read before these writes).
+  // ---- epilogue: finish A into the swizzled LDS tiles ----
+  // (the kind is dispatched once, outside the element loops: a per-element
+  // kind test compiled into ~7 scalar branches per element, 15K cycles)
+  const float us = omega / hf;
+  auto write_tiles = [&](auto mode_c) __attribute__((always_inline)) {
+    constexpr int MODE = decltype(mode_c)::value;  // 0 iALS, 1 U kinds, 2 V kinds, 3 CVaR
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (valid[m]) {
+        const int I = (aoff[m] - lo) >> 5, J = (boff[m] - lo) >> 5;
+        float* tile = tiles + tidx(I, J) * 1024;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int i = acc_row(q, hi);
+          const bool dg = (32 * I + i) == (32 * J + lo);
+          float v = acc[m][q];
+          if constexpr (MODE == 1) v = v * us + (dg ? lam : 0.0f);
+          if constexpr (MODE == 2) v = v + (dg ? lam : 0.0f);
+          if constexpr (MODE == 3)
+            v = assemble(kind, v, a.G[(32 * I + i) * Dp + 32 * J + lo], dg, a.w, lam, hf, omega);
+          tile[sw(i, lo)] = v;
+        }
+      }
+    }
+  };
+  auto store_tiles = [&]() __attribute__((always_inline)) {
+    if constexpr (PARTIAL) {
+      float* sl = a.slabs + (size_t)slab0 * slab_floats;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        if (valid[m]) {
+          const int t = tidx((aoff[m] - lo) >> 5, (boff[m] - lo) >> 5);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) sl[t * 1024 + q * 64 + lane] = acc[m][q];
+        }
+      }
+    } else {
+      if (grad) write_tiles(std::integral_constant<int, 3>{});
+      else if (is_u_kind(kind)) write_tiles(std::integral_constant<int, 1>{});
+      else if (vk) write_tiles(std::integral_constant<int, 2>{});
+      else write_tiles(std::integral_constant<int, 0>{});
+    }
+  };
   lds_barrier();
   mark(0);
   if constexpr (BF) {
@@ -414,7 +521,8 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     }
     if (nchunks > 1) load_bf(1, xa);
     lds_barrier();
-    auto step = [&](int c, float (&xcur)[16], float (&xnxt)[16]) {
+    auto step = [&](int c, float (&xcur)[16], float (&xnxt)[16], auto pc)
+                    __attribute__((always_inline)) {
       const int buf = c & 1;
       const bool ring_more = (tid < R) && (c + 3 < nchunks);
       int nid = -1;
@@ -454,7 +562,27 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
             for (int p = 0; p < 3; ++p) asm volatile("" : "+v"(f[hh][p]));
       };
       const bf16x8* st = reinterpret_cast<const bf16x8*>(stage) + buf * C::GRAN;
-      if (!FRECSYS_SKIP(a.debug_skip, 1)) {
+      if (SB && !FRECSYS_SKIP(a.debug_skip, 1)) {
+        // the wave's column blocks' fragments, each feeding two or more
+        // tiles (per-tile accumulation order as below: bit-identical)
+        {
+          constexpr SbPat P = kSbPat[decltype(pc)::value];
+          constexpr int NX = decltype(pc)::value == 3 ? 3 : 4;
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            bf16x8 fr[NX][3];
+#pragma unroll
+            for (int x = 0; x < NX; ++x)
+#pragma unroll
+              for (int p = 0; p < 3; ++p) fr[x][p] = st[bf_gran<Dp>(p, g, hi, 32 * sbx[x] + lo)];
+#pragma unroll
+            for (int m = 0; m < P.n; ++m) {
+              acc[m] = mfma_x6s(fr[P.pa[m]], fr[P.pb[m]], acc[m]);
+              if (m < 4) split_slot(4 * g + m);
+            }
+          }
+        }
+      } else if (!FRECSYS_SKIP(a.debug_skip, 1)) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           // tiles every wave has: no branch, one basic block with the splits
@@ -485,9 +613,25 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
       }
       lds_barrier();
     };
-    for (int c = 0; c < nchunks; c += 2) {
-      step(c, xa, xb);
-      if (c + 1 < nchunks) step(c + 1, xb, xa);
+    // SB: one copy of the chunk loop per ownership pattern (the tiles'
+    // accumulators then merge once, after the loop, not at every step)
+    auto loop = [&](auto pc) __attribute__((always_inline)) {
+      for (int c = 0; c < nchunks; c += 2) {
+        step(c, xa, xb, pc);
+        if (c + 1 < nchunks) step(c + 1, xb, xa, pc);
+      }
+      store_tiles();
+    };
+    if constexpr (SB) {
+      switch (sb_pattern(wave)) {
+        case 0: loop(std::integral_constant<int, 0>{}); break;
+        case 1: loop(std::integral_constant<int, 1>{}); break;
+        case 2: loop(std::integral_constant<int, 2>{}); break;
+        case 3: loop(std::integral_constant<int, 3>{}); break;
+        default: loop(std::integral_constant<int, 4>{}); break;
+      }
+    } else {
+      loop(std::integral_constant<int, 0>{});
     }
   } else {
     if (nchunks > 0) {
@@ -527,6 +671,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
       if (ring_more) ring_store(c + 2, nid, nsa, nbw);
       lds_barrier();
     }
+    store_tiles();
   }
   mark(1);
   if constexpr (BF) {
@@ -538,49 +683,11 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
   }
   mark(9);
 
-  if (PARTIAL) {
-    float* sl = a.slabs + (size_t)slab0 * slab_floats;
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      if (valid[m]) {
-        const int t = wave + m * NW;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) sl[t * 1024 + q * 64 + lane] = acc[m][q];
-      }
-    }
-    if (tid < Dp) sl[NT * 1024 + tid] = bacc;
+  if (PARTIAL) {  // the tiles went out in store_tiles
+    if (tid < Dp) a.slabs[(size_t)slab0 * slab_floats + NT * 1024 + tid] = bacc;
     return;
   }
 
-  // ---- epilogue: finish A into the swizzled LDS tiles ----
-  // (the kind is dispatched once, outside the element loops: a per-element
-  // kind test compiled into ~7 scalar branches per element, 15K cycles)
-  const float us = omega / hf;
-  auto write_tiles = [&](auto mode_c) __attribute__((always_inline)) {
-    constexpr int MODE = decltype(mode_c)::value;  // 0 iALS, 1 U kinds, 2 V kinds, 3 CVaR
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      if (valid[m]) {
-        const int I = (aoff[m] - lo) >> 5, J = (boff[m] - lo) >> 5;
-        float* tile = tiles + tidx(I, J) * 1024;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int i = acc_row(q, hi);
-          const bool dg = (32 * I + i) == (32 * J + lo);
-          float v = acc[m][q];
-          if constexpr (MODE == 1) v = v * us + (dg ? lam : 0.0f);
-          if constexpr (MODE == 2) v = v + (dg ? lam : 0.0f);
-          if constexpr (MODE == 3)
-            v = assemble(kind, v, a.G[(32 * I + i) * Dp + 32 * J + lo], dg, a.w, lam, hf, omega);
-          tile[sw(i, lo)] = v;
-        }
-      }
-    }
-  };
-  if (grad) write_tiles(std::integral_constant<int, 3>{});
-  else if (is_u_kind(kind)) write_tiles(std::integral_constant<int, 1>{});
-  else if (vk) write_tiles(std::integral_constant<int, 2>{});
-  else write_tiles(std::integral_constant<int, 0>{});
   mark(10);
   if (tid < Dp) {
     float b = bacc;
