@@ -164,6 +164,20 @@ struct frecsys_ctx {
   uint64_t basis_gram[2] = {0, 0};  // gram_ver the basis (T, Q, Q pieces) belongs to
   uint64_t xrot_emb[2] = {0, 0};    // emb_ver of the rotated copy (0: stale / snapshot)
   uint64_t xrot_gram[2] = {0, 0};   // ... and the basis it was rotated into
+  uint64_t xrot_sub[2] = {0, 0};    // ... and the row subset it covers (0: every row)
+  // Row subsets of the forward rotation: the rows of the other side that a
+  // consumer side's history-space entities read (its shard's queue positions
+  // [key0, key1)).  At N ranks a shard's short histories touch a fraction of
+  // the other side, so the replicated rotation shrinks with N.  Built once
+  // per (queue, split point) -- the histories do not change between epochs.
+  int rot_subset_on = 1;            // FRECSYS_ROT_SUBSET=0: rotate every row (A/B)
+  QueueRec* d_hrows[3] = {nullptr, nullptr, nullptr};
+  size_t cap_hrows[3] = {0, 0, 0};
+  int64_t n_hrows[3] = {-1, -1, -1};  // rows in the subset; -1: none (every row)
+  int64_t hrows_key[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}};
+  uint64_t hrows_gen[3] = {0, 0, 0};  // subset id (0: every row)
+  uint8_t* d_mark = nullptr;
+  size_t cap_mark = 0;
   bool dual_used[3] = {false, false, false};  // the side's last solve took history space
   int eager_on = 1;                 // FRECSYS_EAGER=0: no early basis builds (A/B)
   // Basis kind per side: 0 = tridiagonal (G = Q T Q^T, any mu / lambda per
@@ -319,6 +333,7 @@ int build_order(frecsys_ctx* c, int side) {
   c->order_h[side].resize(recs.size());
   for (size_t i = 0; i < recs.size(); ++i) c->order_h[side][i] = recs[i].h;
   c->order_stale[side] = false;
+  c->hrows_key[side][0] = c->hrows_key[side][1] = -1;  // subsets follow the queue
   return FRECSYS_OK;
 }
 
@@ -385,7 +400,8 @@ void emb_written(frecsys_ctx* c, int side) { c->emb_ver[side] = ++c->ver_counter
 // rotated into it (X Q): the inputs of the history-space solve.  Rebuilt
 // only when the Gramian (basis) or the rows (rotation) changed since.
 int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s, int mode = 0,
-                  float mu = 0.f, float lam = 0.f) {
+                  float mu = 0.f, float lam = 0.f, const QueueRec* rows = nullptr,
+                  int64_t nrows = 0, uint64_t sub = 0) {
   const int Dp = c->Dp;
   size_t cap = 0;
   if (!c->q[other]) {
@@ -404,8 +420,11 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s, int 
   const bool need_basis = c->basis_gram[other] == 0 ||
                           c->basis_gram[other] != c->gram_ver[other] || !same_kind;
   const uint64_t xkey = X == c->emb[other] ? c->emb_ver[other] : 0;
+  if (!rows) sub = 0;
   const bool need_rot = need_basis || xkey == 0 || c->xrot_emb[other] != xkey ||
-                        c->xrot_gram[other] != c->gram_ver[other];
+                        c->xrot_gram[other] != c->gram_ver[other] ||
+                        (c->xrot_sub[other] != 0 && c->xrot_sub[other] != sub);
+  const int64_t nrot = rows ? nrows : c->n[other];
   if (s != c->stream5) {
     // an early build of this basis (or one sharing tri_work) may still run
     int rc = join_eager(c, 3, s);
@@ -417,8 +436,9 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s, int 
   if (rc) return rc;
   c->xrot_emb[other] = xkey;
   c->xrot_gram[other] = c->gram_ver[other];
+  c->xrot_sub[other] = sub;
   if (!need_basis) {
-    HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp,
+    HIP_TRY(c, launch_rotate(X, rows, 0, nrot, c->qsplit[other][0], c->xrot[other], Dp,
                              s));
     return FRECSYS_OK;
   }
@@ -441,7 +461,7 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s, int 
                                  c->tri[other], s));
     HIP_TRY(c, launch_split_basis(c->q[other], Dp, 0, c->qsplit[other][0], s));
     HIP_TRY(c, launch_split_basis(c->q[other], Dp, 1, c->qsplit[other][1], s));
-    HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp,
+    HIP_TRY(c, launch_rotate(X, rows, 0, nrot, c->qsplit[other][0], c->xrot[other], Dp,
                              s));
     return FRECSYS_OK;
   }
@@ -456,7 +476,7 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s, int 
     HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp,
                               c->refl[other], tau, s, c->tri_work, c->q[other],
                               c->qsplit[other][0], c->qsplit[other][1]));
-    HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp,
+    HIP_TRY(c, launch_rotate(X, rows, 0, nrot, c->qsplit[other][0], c->xrot[other], Dp,
                              s));
     return FRECSYS_OK;
   }
@@ -464,7 +484,53 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s, int 
                             tau, s, c->tri_work));
   HIP_TRY(c, launch_form_q(c->refl[other], tau, Dp, c->q[other], s, c->qsplit[other][0],
                            c->qsplit[other][1]));
-  HIP_TRY(c, launch_rotate(X, nullptr, 0, c->n[other], c->qsplit[other][0], c->xrot[other], Dp, s));
+  HIP_TRY(c, launch_rotate(X, rows, 0, nrot, c->qsplit[other][0], c->xrot[other], Dp, s));
+  return FRECSYS_OK;
+}
+
+// The rows of `other` that side's history-space entities (its queue
+// positions [q0, q1)) read: a row list when it is well below the whole
+// table, else none (rotate every row).  Marked on the device, compacted on
+// the host once per queue and split point (one synchronisation then).
+int hspace_rows(frecsys_ctx* c, int side, int other, int64_t q0, int64_t q1,
+                const QueueRec** rows, int64_t* nrows, uint64_t* sub) {
+  *rows = nullptr;
+  *nrows = 0;
+  *sub = 0;
+  if (!c->rot_subset_on || q1 <= q0) return FRECSYS_OK;
+  if (c->hrows_key[side][0] != q0 || c->hrows_key[side][1] != q1) {
+    const int64_t no = c->n[other];
+    int rc = ensure(c, &c->d_mark, &c->cap_mark, (size_t)no);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemsetAsync(c->d_mark, 0, (size_t)no, c->stream));
+    HIP_TRY(c, launch_mark_rows(c->d_order[side] + q0, q1 - q0, c->col[side], c->d_mark,
+                                c->stream));
+    std::vector<uint8_t> mark((size_t)no);
+    HIP_TRY(c, hipMemcpyAsync(mark.data(), c->d_mark, (size_t)no, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    std::vector<QueueRec> list;
+    for (int64_t r = 0; r < no; ++r)
+      if (mark[r]) list.push_back(QueueRec{(int32_t)r, 0, 0});
+    c->hrows_key[side][0] = q0;
+    c->hrows_key[side][1] = q1;
+    c->hrows_gen[side] = ++c->ver_counter;
+    if ((double)list.size() > 0.7 * (double)no) {
+      c->n_hrows[side] = -1;  // most of the table: one plain pass over it
+    } else {
+      rc = ensure(c, &c->d_hrows[side], &c->cap_hrows[side], std::max<size_t>(list.size(), 1));
+      if (rc) return rc;
+      if (!list.empty())
+        HIP_TRY(c, hipMemcpy(c->d_hrows[side], list.data(), sizeof(QueueRec) * list.size(),
+                             hipMemcpyHostToDevice));
+      c->n_hrows[side] = (int64_t)list.size();
+    }
+  }
+  if (c->n_hrows[side] >= 0) {
+    *rows = c->d_hrows[side];
+    *nrows = c->n_hrows[side];
+    *sub = c->hrows_gen[side];
+  }
   return FRECSYS_OK;
 }
 
@@ -476,14 +542,19 @@ int maybe_start_eager(frecsys_ctx* c, int g) {
   if (!c->eager_on || c->dual_serial || !c->dual_on || c->Dp < 64 || c->dual_max_h <= 0 ||
       !c->dual_used[consumer] || c->eager_pending[g])
     return FRECSYS_OK;
+  // the consumer's last row subset (its next solve checks it still applies)
+  const bool subset = c->n_hrows[consumer] >= 0 && c->hrows_key[consumer][0] >= 0;
+  const QueueRec* rows = subset ? c->d_hrows[consumer] : nullptr;
+  const uint64_t sub = subset ? c->hrows_gen[consumer] : 0;
   if (c->basis_gram[g] == c->gram_ver[g] && c->xrot_emb[g] == c->emb_ver[g] &&
       c->xrot_gram[g] == c->gram_ver[g] && c->basis_mode[g] == c->want_mode[g] &&
-      c->basis_mu[g] == c->want_mu[g] && c->basis_lam[g] == c->want_lam[g])
+      c->basis_mu[g] == c->want_mu[g] && c->basis_lam[g] == c->want_lam[g] &&
+      (c->xrot_sub[g] == 0 || c->xrot_sub[g] == sub))
     return FRECSYS_OK;  // already current
   HIP_TRY(c, hipEventRecord(c->ev_pre5, c->stream));
   HIP_TRY(c, hipStreamWaitEvent(c->stream5, c->ev_pre5, 0));
   int rc = prepare_basis(c, g, c->emb[g], c->stream5, c->want_mode[g], c->want_mu[g],
-                         c->want_lam[g]);
+                         c->want_lam[g], rows, subset ? c->n_hrows[consumer] : 0, sub);
   if (rc) return rc;
   HIP_TRY(c, hipEventRecord(c->ev_eager[g], c->stream5));
   c->eager_pending[g] = true;
@@ -839,6 +910,7 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
     return bail(fail(c, FRECSYS_ERR_HIP, "hipEventCreate failed (early builds)"));
   if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
   if (const char* v = getenv("FRECSYS_EAGER")) c->eager_on = atoi(v);
+  if (const char* v = getenv("FRECSYS_ROT_SUBSET")) c->rot_subset_on = atoi(v);
   if (const char* v = getenv("FRECSYS_CHOL_BASIS")) c->chol_basis_on = atoi(v);
   // d-space / history-space crossover: by flops h = d, but at Dp <= 256 the
   // d-space kernel overtakes the TH = 8 bucket (225 < h <= 256) in time (epoch
@@ -912,6 +984,9 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (c->gsplit) (void)hipFree(c->gsplit);
   for (int s = 0; s < 3; ++s)
     if (c->out_rot[s]) (void)hipFree(c->out_rot[s]);
+  for (int s = 0; s < 3; ++s)
+    if (c->d_hrows[s]) (void)hipFree(c->d_hrows[s]);
+  if (c->d_mark) (void)hipFree(c->d_mark);
   if (c->dual_table) (void)hipFree(c->dual_table);
   if (c->tri_work) (void)hipFree(c->tri_work);
   if (c->chol_work) (void)hipFree(c->chol_work);
@@ -1467,8 +1542,13 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       c->want_mode[other] = bmode;
       c->want_mu[other] = bmu;
       c->want_lam[other] = blam;
+      const QueueRec* hrows = nullptr;
+      int64_t nhrows = 0;
+      uint64_t hsub = 0;
+      rc = hspace_rows(c, side, other, n_dspace, n_nonempty, &hrows, &nhrows, &hsub);
+      if (rc) return rc;
       size_t k = ktimer_begin(c, pre + ".basis", c->stream);
-      rc = prepare_basis(c, other, a.X, c->stream, bmode, bmu, blam);
+      rc = prepare_basis(c, other, a.X, c->stream, bmode, bmu, blam, hrows, nhrows, hsub);
       if (rc) return rc;
       ktimer_end(c, k, c->stream);
       if (n_dspace > 0) {

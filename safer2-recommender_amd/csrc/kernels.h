@@ -203,6 +203,10 @@ hipError_t launch_chol_basis(const float* G, int Dp, float mu, float lam, float*
 // for rows r0..r0+n-1, or for the entities rows[0..n) when rows != nullptr
 // (Y: ld Dp; X: ld Dp, or with x_blocked the position-blocked layout of
 // DualArgs::out_rot, X row r = position r).  Dp = 64 .. 256, 512, 1024.
+// Rows of the other side that a side's history-space entities read (the
+// forward rotation's subset): mark[col[p]] = 1 over their histories.
+hipError_t launch_mark_rows(const QueueRec* order, int64_t n, const int32_t* col, uint8_t* mark,
+                            hipStream_t s);
 hipError_t launch_rotate(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
                          const void* bsplit, float* Y, int Dp, hipStream_t s, int x_blocked = 0);
 // Dp = 512 / 1024: qpart[b * n + r] = sum over the columns of 128-block b of

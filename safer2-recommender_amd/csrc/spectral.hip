@@ -486,7 +486,10 @@ __global__ void __launch_bounds__(256)
   const int C0 = cbk * CB + cg * CW;
   const int64_t pos = base + 32 * R + lo;  // my A row (position)
   const bool pv = pos < n;
-  const float* xr = X + (x_blocked ? 0 : (r0 + (pv ? pos : base)) * DP);
+  // X row: the entity rows[p] with a row list (forward rotation of a row
+  // subset), else position r0 + p (x_blocked: the position-blocked layout)
+  const int64_t xp = pv ? pos : base;
+  const float* xr = X + (x_blocked ? 0 : (rows ? (int64_t)rows[xp].entity : r0 + xp) * DP);
   f32x16 acc[CW];
 #pragma unroll
   for (int j = 0; j < CW; ++j) acc[j] = f32x16{0.f};
@@ -754,7 +757,8 @@ __global__ void __launch_bounds__(256)
   for (int t = 0; t < RT; ++t) {
     pos[t] = base + 32 * (R * RT + t) + lo;
     pv[t] = pos[t] < n;
-    xr[t] = X + (x_blocked ? 0 : (r0 + (pv[t] ? pos[t] : base)) * DP);
+    const int64_t xp = pv[t] ? pos[t] : base;
+    xr[t] = X + (x_blocked ? 0 : (rows ? (int64_t)rows[xp].entity : r0 + xp) * DP);
   }
   f32x16 acc[RT][CW];
 #pragma unroll
@@ -979,6 +983,22 @@ hipError_t launch_rotate(const float* X, const QueueRec* rows, int64_t r0, int64
     case 1024: return launch_rotate_t<1024>(X, rows, r0, n, B, Y, s, x_blocked);
     default: return hipErrorInvalidValue;
   }
+}
+
+namespace {
+__global__ void __launch_bounds__(256) mark_rows_kernel(const QueueRec* __restrict__ order,
+                                                        const int32_t* __restrict__ col,
+                                                        uint8_t* __restrict__ mark) {
+  const QueueRec r = order[blockIdx.x];
+  for (int64_t k = threadIdx.x; k < r.h; k += 256) mark[col[r.p0 + k]] = 1;
+}
+}  // namespace
+
+hipError_t launch_mark_rows(const QueueRec* order, int64_t n, const int32_t* col, uint8_t* mark,
+                            hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mark_rows_kernel, dim3((unsigned)n), dim3(256), 0, s, order, col, mark);
+  return hipGetLastError();
 }
 
 hipError_t launch_rotate_quad(const float* X, int64_t r0, int64_t n, const void* bsplit,
