@@ -196,6 +196,7 @@ struct frecsys_ctx {
   hipEvent_t ev_eager[2] = {nullptr, nullptr};
   bool eager_pending[2] = {false, false};
   int dual_max_h = 256;  // longest h_eff on the history-space path (set per Dp at create)
+  int dual_max_h_side[3] = {256, 256, 256};  // per solved side (FRECSYS_DUAL_MAX_H_USER / _ITEM)
   int dual_serial = 0;  // FRECSYS_DUAL_SERIAL=1: no stream overlap (profiling)
   int debug_skip = 0;   // FRECSYS_DEBUG_SKIP ablation mask (-DFRECSYS_ABLATION builds only)
   // per-kernel event pairs, resolved after the call's final synchronisation
@@ -933,6 +934,11 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   }
   if (const char* v = getenv("FRECSYS_WIDE_WS_MB")) c->wide_ws_mb = std::max(1, atoi(v));
   c->dual_max_h = std::min(c->dual_max_h, 32 * kDualMaxTiles);
+  for (int t = 0; t < 3; ++t) c->dual_max_h_side[t] = c->dual_max_h;
+  if (const char* v = getenv("FRECSYS_DUAL_MAX_H_USER"))
+    c->dual_max_h_side[0] = std::min(atoi(v), 32 * kDualMaxTiles);
+  if (const char* v = getenv("FRECSYS_DUAL_MAX_H_ITEM"))
+    c->dual_max_h_side[1] = std::min(atoi(v), 32 * kDualMaxTiles);
   for (int s = 0; s < 2; ++s) {
     const size_t rows = (size_t)std::max<int64_t>(c->n[s], 1);
     if (hipMalloc((void**)&c->emb[s], sizeof(float) * rows * Dp) != hipSuccess ||
@@ -1507,8 +1513,8 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
     for (int64_t i = 0; i < c->n[side] && m_spd; ++i) m_spd = p->entity_reg[i] + base > 0.0f;
   }
   const bool dual = c->dual_on && !force_dspace && m_spd && !grad && c->Dp >= 64 &&
-                    c->dual_max_h > 0 && (int64_t)hs.size() == c->order_n[side];
-  const int64_t n_dspace = dual ? first_le(c->dual_max_h) : a.n_rows;
+                    c->dual_max_h_side[side] > 0 && (int64_t)hs.size() == c->order_n[side];
+  const int64_t n_dspace = dual ? first_le(c->dual_max_h_side[side]) : a.n_rows;
   c->dual_used[side] = dual;
   if (side < 2) emb_written(c, side);
   const int64_t n_nonempty = dual ? first_le(0) : a.n_rows;
