@@ -500,8 +500,12 @@ int hspace_rows(frecsys_ctx* c, int side, int other, int64_t q0, int64_t q1,
   *sub = 0;
   if (!c->rot_subset_on || q1 <= q0) return FRECSYS_OK;
   if (c->hrows_key[side][0] != q0 || c->hrows_key[side][1] != q1) {
+    // an early build may still be rotating with the old list (stream5): the
+    // synchronisation below then covers it before the list is rewritten
+    int rc = join_eager(c, 3, c->stream);
+    if (rc) return rc;
     const int64_t no = c->n[other];
-    int rc = ensure(c, &c->d_mark, &c->cap_mark, (size_t)no);
+    rc = ensure(c, &c->d_mark, &c->cap_mark, (size_t)no);
     if (rc) return rc;
     HIP_TRY(c, hipMemsetAsync(c->d_mark, 0, (size_t)no, c->stream));
     HIP_TRY(c, launch_mark_rows(c->d_order[side] + q0, q1 - q0, c->col[side], c->d_mark,
