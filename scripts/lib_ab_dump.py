@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import frecsys_hip as fh  # noqa: E402
 from frecsys_hip.data import SynthShape, synthetic  # noqa: E402
 
-os.environ["FRECSYS_DUAL"] = "0"
+os.environ.setdefault("FRECSYS_DUAL", "0")  # FRECSYS_DUAL=1: the history-space path too
 os.environ["FRECSYS_SPLIT_ROWS"] = "64"
 fh.load_library(sys.argv[1])
 shape = SynthShape(20_000, 5_000, 1_000_000, min_uc=5)
