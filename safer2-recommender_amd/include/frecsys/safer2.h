@@ -233,7 +233,9 @@ class SAFER2Recommender : public detail::DeviceModel {
       tv += ms(c, d);
       tl += ms(d, now());
       VectorXf wl(num_users_);
-      for (int64_t u = 0; u < num_users_; ++u) wl[u] = dual_weight_[u] * user_loss_[u];
+      ThreadPool::Get().ParallelFor(num_users_, 16384, [&](int64_t lo, int64_t hi) {
+        for (int64_t u = lo; u < hi; ++u) wl[u] = dual_weight_[u] * user_loss_[u];
+      });
       LOG(INFO) << "Weighted Loss: " << wl.mean();                // safer2.h:300-301
       if (print_varstats_) {
         PrintVarStats(alpha_);
@@ -335,7 +337,9 @@ class SAFER2Recommender : public detail::DeviceModel {
   void StepV(const Dataset& data) {
     (void)data;
     std::vector<float> nu((size_t)num_users_);
-    for (int64_t u = 0; u < num_users_; ++u) nu[u] = dual_weight_[u] / user_history_size_[u];
+    ThreadPool::Get().ParallelFor(num_users_, 16384, [&](int64_t lo, int64_t hi) {
+      for (int64_t u = lo; u < hi; ++u) nu[u] = dual_weight_[u] / user_history_size_[u];
+    });
     dev_->Gramian(DeviceContext::USER, dual_weight_.data(), ++weight_epoch_);  // :504-509
     frecsys_solve_params p = solve_params(FRECSYS_KIND_WEIGHTED_V, regularization_,
                                           unobserved_weight_);
