@@ -1,6 +1,6 @@
 # Round-end check on one GPU box: the whole -m gpu suite, smoke(), the default bench line.
 set -o pipefail
-OUT=gpurun_out/final2
+OUT=gpurun_out/${1:-final2}
 mkdir -p $OUT
 timeout -k 10 780 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo pytest failed; tail -30 $OUT/pytest.log; exit 1; }
 tail -2 $OUT/pytest.log
