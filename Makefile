@@ -17,7 +17,7 @@ HIPCC    ?= /opt/rocm/bin/hipcc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 CXXFLAGS := -O3 -std=c++17 -Wall -I include -I $(PKG)/include -pthread
 
-HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/solve_rr.hip $(CSRC)/dual.hip $(CSRC)/spectral.hip $(CSRC)/gramian.hip \
+HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/dual.hip $(CSRC)/spectral.hip $(CSRC)/gramian.hip \
             $(CSRC)/loss.hip $(CSRC)/wide.hip $(CSRC)/topk.hip $(CSRC)/pp.hip \
             $(CSRC)/capi.hip
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))

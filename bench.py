@@ -410,6 +410,10 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
     item = item_gather_fabric(pmc, si_ms, ni, Dp)
     if item:
         res["item_gather_fabric"] = item
+    # the silent slow path (a side rerun in d-space after a history-space
+    # pivot failure or a tagged-poll timeout), over the whole run incl. warmup
+    res["hspace_reruns"] = ctx.counter("hspace_reruns")
+    res["tagged_timeouts"] = ctx.counter("tagged_timeouts")
     if spec["model"] != "ials":
         res["mean_dual_weight"] = model.mean_weight()
     if cpu_s > 0 and world == 1 and rank == 0:
@@ -495,7 +499,8 @@ def main():
             "frecsys_env": env,
         }
         for k in ("u_halfstep_solve_updates_per_s", "kernel_ms_per_epoch", "roofline", "paths",
-                  "gather_roofline", "loss_gather_roofline", "cpu_baseline"):
+                  "gather_roofline", "loss_gather_roofline", "cpu_baseline", "hspace_reruns",
+                  "tagged_timeouts"):
             line[k] = head[k]
         line["workloads"] = {r["workload"]: r for r in extras}
         print(json.dumps(line), flush=True)

@@ -240,6 +240,20 @@ int frecsys_eval_topk(frecsys_ctx* ctx, int32_t k, int32_t* topk);
  * by the solves are left untouched. */
 int frecsys_train_stats(frecsys_ctx* ctx, double* observed, double* unobserved,
                         float* user_norm2, float* item_norm2);
+/* Sum over every row of `side` of ||X_r - snapshot_r||^2 (double), against
+ * the snapshot frecsys_snapshot took: the residual norms of
+ * --print_residual_stats, squared (StepU's sum of squared row changes,
+ * safer2.h:475-478 / erm_mf.h:434-437; StepV's (V - V_prev).norm(),
+ * safer2.h:550-553 / erm_mf.h:508-511 / cvar_mf.h:533-536). */
+int frecsys_snapshot_residual(frecsys_ctx* ctx, int32_t side, double* sq);
+/* Cumulative event counters of the context (never reset):
+ *   "hspace_reruns"   solves of a side rerun on the d-space path after a
+ *                     history-space pivot failure (a silent slow path);
+ *   "tagged_timeouts" device polls of the tagged-word exchange of the
+ *                     tridiagonalisation that timed out (each one poisons
+ *                     the basis and forces a rerun).
+ * No reference counterpart (diagnostics of the MI355X path). */
+int frecsys_counter(frecsys_ctx* ctx, const char* what, int64_t* value);
 /* Block until all queued device work is done (all calls already do). */
 int frecsys_synchronize(frecsys_ctx* ctx);
 

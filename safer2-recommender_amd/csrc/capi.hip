@@ -81,6 +81,10 @@ struct frecsys_ctx {
   size_t cap_quad = 0;
   unsigned long long* d_fail = nullptr;
   unsigned int* d_counter = nullptr;
+  // cumulative event counters (frecsys_counter): [0] tagged-word polls that
+  // timed out on the device (common.h tpoll); history-space reruns on host
+  unsigned int* d_events = nullptr;
+  int64_t hspace_reruns = 0;
   // per side: the rank's entities in decreasing-history order (LPT queue)
   QueueRec* d_order[3] = {nullptr, nullptr, nullptr};
   int64_t order_n[3] = {0, 0, 0};
@@ -175,6 +179,16 @@ struct frecsys_ctx {
   size_t cap_hrows[3] = {0, 0, 0};
   int64_t n_hrows[3] = {-1, -1, -1};  // rows in the subset; -1: none (every row)
   int64_t hrows_key[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}};
+  // Prefix sums over each side's queue of h_eff, h_eff^2, h_eff^3 and the
+  // non-empty count (two variants: with / without the ProjectV tail rows):
+  // the frecsys_work accounting of any queue range in O(1) instead of a host
+  // loop over the entities on every solve.  Rebuilt with the queue.
+  struct WorkPrefix {
+    bool valid = false;
+    std::vector<double> h1, h2, h3;
+    std::vector<int64_t> nz;
+  };
+  WorkPrefix wprefix[3][2];
   uint64_t hrows_gen[3] = {0, 0, 0};  // subset id (0: every row)
   uint8_t* d_mark = nullptr;
   size_t cap_mark = 0;
@@ -244,9 +258,9 @@ void add_work(frecsys_ctx* c, const std::string& key, double flops, double bytes
 // SURVEY 8(d) per entity of h assembly rows at dim d: d-space SYRK
 // h d (d+1) and LLT d^3/3 + 2 d^2 flops; gather bytes h d 4 (rows) + h 4
 // (ids) + 8 (row offset) + d 4 (the solution written).
-double dspace_syrk_flops(double h, double d) { return h * d * (d + 1.0); }
+// (SYRK and gather are linear in h: summed from the queue prefix sums,
+// heff_sums below.)
 double dspace_solve_flops(double d) { return d * d * d / 3.0 + 2.0 * d * d; }
-double gather_bytes(double h, double d) { return h * d * 4.0 + h * 4.0 + 8.0 + d * 4.0; }
 
 template <typename T>
 int ensure(frecsys_ctx* c, T** p, size_t* cap, size_t count) {
@@ -334,8 +348,44 @@ int build_order(frecsys_ctx* c, int side) {
   c->order_h[side].resize(recs.size());
   for (size_t i = 0; i < recs.size(); ++i) c->order_h[side][i] = recs[i].h;
   c->order_stale[side] = false;
+  c->wprefix[side][0].valid = c->wprefix[side][1].valid = false;
   c->hrows_key[side][0] = c->hrows_key[side][1] = -1;  // subsets follow the queue
   return FRECSYS_OK;
+}
+
+// Sums of h_eff, h_eff^2, h_eff^3 and of the non-empty entities over queue
+// positions [lo, hi) of `side` (vq: the V kinds' tail-quirk h_eff).
+struct HeffSums {
+  double h1 = 0, h2 = 0, h3 = 0;
+  int64_t nz = 0;
+};
+HeffSums heff_sums(frecsys_ctx* c, int side, bool vq, int64_t lo, int64_t hi) {
+  frecsys_ctx::WorkPrefix& p = c->wprefix[side][vq ? 1 : 0];
+  const std::vector<int32_t>& hs = c->order_h[side];
+  if (!p.valid || p.h1.size() != hs.size() + 1) {
+    const size_t n = hs.size();
+    p.h1.assign(n + 1, 0.0);
+    p.h2.assign(n + 1, 0.0);
+    p.h3.assign(n + 1, 0.0);
+    p.nz.assign(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) {
+      const int64_t h0 = hs[i];
+      const double h = (double)((vq && c->quirks && h0 > 128 && (h0 % 128) != 0)
+                                    ? h0 + 128 - (h0 % 128) : h0);
+      p.h1[i + 1] = p.h1[i] + h;
+      p.h2[i + 1] = p.h2[i] + h * h;
+      p.h3[i + 1] = p.h3[i] + h * h * h;
+      p.nz[i + 1] = p.nz[i] + (h > 0 ? 1 : 0);
+    }
+    p.valid = true;
+  }
+  HeffSums s;
+  if (hi <= lo) return s;
+  s.h1 = p.h1[hi] - p.h1[lo];
+  s.h2 = p.h2[hi] - p.h2[lo];
+  s.h3 = p.h3[hi] - p.h3[lo];
+  s.nz = p.nz[hi] - p.nz[lo];
+  return s;
 }
 
 // Long-history split of the d-space queue prefix [0, n): entities with
@@ -476,13 +526,13 @@ int prepare_basis(frecsys_ctx* c, int other, const float* X, hipStream_t s, int 
     // Q rows and their split images formed inside the reduction's launch
     HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp,
                               c->refl[other], tau, s, c->tri_work, c->q[other],
-                              c->qsplit[other][0], c->qsplit[other][1]));
+                              c->qsplit[other][0], c->qsplit[other][1], c->d_events));
     HIP_TRY(c, launch_rotate(X, rows, 0, nrot, c->qsplit[other][0], c->xrot[other], Dp,
                              s));
     return FRECSYS_OK;
   }
   HIP_TRY(c, launch_tridiag(c->gram[other], Dp, c->tri[other], c->tri[other] + Dp, c->refl[other],
-                            tau, s, c->tri_work));
+                            tau, s, c->tri_work, nullptr, nullptr, nullptr, c->d_events));
   HIP_TRY(c, launch_form_q(c->refl[other], tau, Dp, c->q[other], s, c->qsplit[other][0],
                            c->qsplit[other][1]));
   HIP_TRY(c, launch_rotate(X, rows, 0, nrot, c->qsplit[other][0], c->xrot[other], Dp, s));
@@ -952,8 +1002,10 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
     (void)hipMemsetAsync(c->gram[s], 0, sizeof(float) * Dp * Dp, c->stream);
   }
   if (hipMalloc((void**)&c->d_fail, sizeof(unsigned long long)) != hipSuccess ||
-      hipMalloc((void**)&c->d_counter, sizeof(unsigned int)) != hipSuccess)
+      hipMalloc((void**)&c->d_counter, sizeof(unsigned int)) != hipSuccess ||
+      hipMalloc((void**)&c->d_events, 4 * sizeof(unsigned int)) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_HIP, "hipMalloc failed"));
+  (void)hipMemsetAsync(c->d_events, 0, 4 * sizeof(unsigned int), c->stream);
   c->bounds[0] = {0, c->n[0]};
   c->bounds[1] = {0, c->n[1]};
   if (hipStreamSynchronize(c->stream) != hipSuccess)
@@ -983,6 +1035,7 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->d_fail) (void)hipFree(c->d_fail);
   if (c->d_counter) (void)hipFree(c->d_counter);
+  if (c->d_events) (void)hipFree(c->d_events);
   for (int s = 0; s < 3; ++s)
     if (c->d_order[s]) (void)hipFree(c->d_order[s]);
   for (int s = 0; s < 2; ++s) {
@@ -1337,7 +1390,7 @@ namespace {
 // the HBM-workspace batches of wide.hip at Dp = 512 / 1024.
 int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
                   const std::function<int64_t(int64_t)>& heff, hipStream_t s,
-                  const std::string& pre, bool can_split) {
+                  const std::string& pre, bool can_split, int side, bool vq) {
   if (wide_dim(c->Dp)) {
     const size_t slot = wide_slot_floats(c->Dp);
     const int64_t budget = (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (slot * sizeof(float)));
@@ -1353,16 +1406,12 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
     const size_t k = ktimer_begin(c, pre + ".dspace", s);
     HIP_TRY(c, launch_wide_solve(c->Dp, ap, c->wide_ws, batch, s));
     ktimer_end(c, k, s);
-    double f = 0, b = 0;
-    int64_t ne = 0;
-    for (int64_t i = 0; i < ap.n_rows; ++i) {
-      const double h = (double)heff(hs[i]);
-      if (h <= 0) continue;  // untouched
-      f += dspace_syrk_flops(h, c->dim) + dspace_solve_flops(c->dim);
-      b += gather_bytes(h, c->dim);
-      ++ne;
-    }
-    add_work(c, pre + ".dspace", f, b, ne);  // slabs + batches: one timed call
+    // SURVEY 8(d) per entity: dspace_syrk_flops + dspace_solve_flops, gather_bytes
+    // (empty histories untouched); both linear in h, so from the prefix sums
+    const double d = c->dim;
+    const HeffSums hsum = heff_sums(c, side, vq, 0, ap.n_rows);
+    add_work(c, pre + ".dspace", d * (d + 1.0) * hsum.h1 + hsum.nz * dspace_solve_flops(d),
+             (d * 4.0 + 4.0) * hsum.h1 + hsum.nz * (8.0 + d * 4.0), hsum.nz);  // one timed call
     return FRECSYS_OK;
   }
   if (can_split) {
@@ -1386,25 +1435,15 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
   HIP_TRY(c, launch_solve(c->Dp, ap, s));
   ktimer_end(c, k, s);
   {  // the split entities' SYRK is the split kernel's work, their solve this one's
-    double f = 0, b = 0, fs = 0, bs = 0;
-    int64_t ne = 0, nsplit = 0;
-    for (int64_t i = 0; i < ap.n_rows; ++i) {
-      const double h = (double)heff(hs[i]);
-      if (h <= 0) continue;
-      ++ne;
-      if (i < ap.n_split) {
-        fs += dspace_syrk_flops(h, c->dim);
-        bs += h * c->dim * 4.0 + h * 4.0;
-        f += dspace_solve_flops(c->dim);
-        b += 8.0 + c->dim * 4.0;
-        ++nsplit;
-      } else {
-        f += dspace_syrk_flops(h, c->dim) + dspace_solve_flops(c->dim);
-        b += gather_bytes(h, c->dim);
-      }
-    }
-    add_work(c, pre + ".dspace", f, b, ne);
-    if (ap.n_work > 0) add_work(c, pre + ".split", fs, bs, nsplit);
+    const double d = c->dim;
+    const HeffSums sp = heff_sums(c, side, vq, 0, ap.n_split);
+    const HeffSums rest = heff_sums(c, side, vq, ap.n_split, ap.n_rows);
+    const int64_t ne = sp.nz + rest.nz;
+    add_work(c, pre + ".dspace",
+             d * (d + 1.0) * rest.h1 + (double)ne * dspace_solve_flops(d),
+             (d * 4.0 + 4.0) * rest.h1 + (double)ne * (8.0 + d * 4.0), ne);
+    if (ap.n_work > 0)
+      add_work(c, pre + ".split", d * (d + 1.0) * sp.h1, (d * 4.0 + 4.0) * sp.h1, sp.nz);
   }
   if (dprof) {  // diagnostics: mean cycles per entity and phase
     unsigned long long hp[16];
@@ -1528,7 +1567,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
     ScopedTimer t(c, names[side]);
     if (!dual || n_dspace >= n_nonempty) {
       rc = launch_dspace(c, a, hs, heff, c->stream, pre,
-                         c->Dp >= 32 && (int64_t)hs.size() == c->order_n[side]);
+                         c->Dp >= 32 && (int64_t)hs.size() == c->order_n[side], side, vkind);
       if (rc) return rc;
     } else {
       // d-space solve of the long histories on stream2, concurrently with
@@ -1565,7 +1604,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
         HIP_TRY(c, hipStreamWaitEvent(s2, c->ev_fork, 0));
         SolveArgs ap = a;
         ap.n_rows = n_dspace;
-        rc = launch_dspace(c, ap, hs, heff, s2, pre, true);
+        rc = launch_dspace(c, ap, hs, heff, s2, pre, true, side, vkind);
         if (rc) return rc;
         HIP_TRY(c, hipEventRecord(c->ev_join, s2));
       }
@@ -1640,14 +1679,12 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       ktimer_end(c, k, c->stream);
       {  // h x h system per entity: S = I + Z D^-1 Z^T (h^2 d), its LLT (h^3 / 3),
          // the recurrence and Y^T z (4 h d); rows read twice, the LDL row
-        double f = 0, b = 0;
         const double dd = c->dim;
-        for (int64_t i = n_dspace; i < n_nonempty; ++i) {
-          const double h = (double)heff(hs[i]);
-          f += h * h * dd + h * h * h / 3.0 + 4.0 * h * dd;
-          b += 2.0 * h * dd * 4.0 + h * 4.0 + 8.0 + 3.0 * dd * 4.0 + dd * 4.0;
-        }
-        add_work(c, pre + ".hspace", f, b, n_nonempty - n_dspace);
+        const HeffSums hsum = heff_sums(c, side, vkind, n_dspace, n_nonempty);
+        const double ne = (double)(n_nonempty - n_dspace);
+        add_work(c, pre + ".hspace", hsum.h2 * dd + hsum.h3 / 3.0 + 4.0 * hsum.h1 * dd,
+                 (2.0 * dd * 4.0 + 4.0) * hsum.h1 + ne * (8.0 + 3.0 * dd * 4.0 + dd * 4.0),
+                 n_nonempty - n_dspace);
       }
       k = ktimer_begin(c, pre + ".rotate", c->stream);
       HIP_TRY(c, launch_rotate(c->out_rot[side], a.order + n_dspace, 0, n_nonempty - n_dspace,
@@ -1690,7 +1727,10 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
     }
   }
   if (f != none && dual && (collective || n_dspace < n_nonempty)) {
-    // a history-space pivot failed: the verdict is the d-space solve's
+    // a history-space pivot failed (or a poisoned basis after a tagged-poll
+    // timeout): the verdict is the d-space solve's.  Counted (frecsys_counter
+    // "hspace_reruns"): the whole side pays a d-space solve
+    ++c->hspace_reruns;
     return solve_side_impl(c, side, p, true);
   }
   if (f != none) {
@@ -2091,6 +2131,44 @@ int frecsys_debug_basis(frecsys_ctx* c, int32_t side, float* q, float* diag, flo
 
 int32_t frecsys_history_space_max_h(const frecsys_ctx* c) {
   return c && c->dual_on && c->Dp >= 64 ? c->dual_max_h : 0;
+}
+
+int frecsys_counter(frecsys_ctx* c, const char* what, int64_t* value) {
+  if (!c || !what || !value) return fail(c, FRECSYS_ERR_INVALID, "counter: bad arguments");
+  if (!strcmp(what, "hspace_reruns")) {
+    *value = c->hspace_reruns;
+    return FRECSYS_OK;
+  }
+  if (!strcmp(what, "tagged_timeouts")) {
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipStreamSynchronize(c->stream5));
+    unsigned ev[4] = {0, 0, 0, 0};
+    HIP_TRY(c, hipMemcpyAsync(ev, c->d_events, sizeof(ev), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    *value = (int64_t)ev[0];
+    return FRECSYS_OK;
+  }
+  return fail(c, FRECSYS_ERR_INVALID, std::string("counter: unknown counter ") + what);
+}
+
+int frecsys_snapshot_residual(frecsys_ctx* c, int32_t side, double* sq) {
+  if (!c || side < 0 || side > 1 || !sq) return fail(c, FRECSYS_ERR_INVALID, "snapshot_residual: bad arguments");
+  if (!c->snap[side]) return fail(c, FRECSYS_ERR_INVALID, "snapshot_residual: no snapshot taken");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int64_t n = c->n[side];
+  int rc = ensure(c, &c->d_rows, &c->cap_rows, (size_t)std::max<int64_t>(n, 1));
+  if (rc) return rc;
+  *sq = 0.0;
+  if (n == 0) return FRECSYS_OK;
+  HIP_TRY(c, launch_row_diff2(c->emb[side], c->snap[side], n, c->Dp, c->d_rows, c->stream));
+  std::vector<float> h((size_t)n);
+  HIP_TRY(c, hipMemcpyAsync(h.data(), c->d_rows, sizeof(float) * n, hipMemcpyDeviceToHost,
+                            c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  double s = 0.0;
+  for (float v : h) s += (double)v;
+  *sq = s;
+  return FRECSYS_OK;
 }
 
 int frecsys_timing_reset(frecsys_ctx* c) {

@@ -183,16 +183,20 @@ __device__ __forceinline__ void tstore(unsigned long long* p, unsigned tag, floa
   __hip_atomic_store(p, ((unsigned long long)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-// Bounded wait (~2^24 polls): on timeout *err (if given) is set and 0 / NaN
-// (nan_on_timeout) returned, so a caller never spins forever.
+// Bounded wait (~2^24 polls): on timeout *err (if given) is set, *tcount
+// (if given: the context's cumulative timeout counter, frecsys_counter
+// "tagged_timeouts") incremented and 0 / NaN (nan_on_timeout) returned, so a
+// caller never spins forever.
 __device__ __forceinline__ float tpoll(const unsigned long long* p, unsigned tag, int* err,
-                                       bool nan_on_timeout = false) {
+                                       bool nan_on_timeout = false,
+                                       unsigned* tcount = nullptr) {
   unsigned spins = 0;
   while (true) {
     const unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((unsigned)(v >> 32) == tag) return __uint_as_float((unsigned)v);
     if (++spins > (1u << 24)) {
       if (err) atomicExch(err, 1);
+      if (tcount) atomicAdd(tcount, 1u);
       return nan_on_timeout ? __builtin_nanf("") : 0.0f;
     }
     if (err && (spins & 255) == 0 &&
@@ -222,7 +226,7 @@ __device__ __forceinline__ void qrows_worker(int wid, int n, int nsteps,
                                              const unsigned long long* vt,
                                              const unsigned long long* tt, float* Q,
                                              bf16x8* img_q, bf16x8* img_qt, float* vsh,
-                                             float* tau2) {
+                                             float* tau2, unsigned* tcount) {
   constexpr int TPR = NT / 32, NC = NMAX / TPR;
   const int tid = threadIdx.x, rr = tid / TPR, cs = tid % TPR;
   const int row = 32 * wid + rr;
@@ -232,8 +236,8 @@ __device__ __forceinline__ void qrows_worker(int wid, int n, int nsteps,
   for (int k = 0; k < nsteps; ++k) {
     float* v = vsh + (k & 1) * NMAX;
     for (int r = tid; r < NMAX; r += NT)
-      v[r] = (r > k && r < n) ? tpoll(vt + (size_t)k * n + r, k + 1, nullptr, true) : 0.0f;
-    if (tid == 0) tau2[k & 1] = tpoll(tt + k, k + 1, nullptr, true);
+      v[r] = (r > k && r < n) ? tpoll(vt + (size_t)k * n + r, k + 1, nullptr, true, tcount) : 0.0f;
+    if (tid == 0) tau2[k & 1] = tpoll(tt + k, k + 1, nullptr, true, tcount);
     __syncthreads();
     const float tau = tau2[k & 1];
     if (tau != 0.0f) {  // workgroup-uniform

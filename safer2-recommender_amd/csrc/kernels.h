@@ -180,7 +180,8 @@ hipError_t launch_dual(int tiles, const DualArgs& a, hipStream_t s);
 // img_q / img_qt the split images of Q and Q^T (launch_split_basis's layout).
 hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
                           float* tau, hipStream_t s, float* work = nullptr, float* Q = nullptr,
-                          void* img_q = nullptr, void* img_qt = nullptr);
+                          void* img_q = nullptr, void* img_qt = nullptr,
+                          unsigned* tcount = nullptr);
 bool tridiag_forms_q(int Dp);
 size_t tridiag_work_floats(int Dp);
 // Q = H_0 H_1 ... H_{Dp-3} from the reflectors, row-major Dp x Dp; with
@@ -285,7 +286,8 @@ size_t wide_tridiag_work_floats(int Dp);
 bool wide_tridiag_tagged();
 hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
                                float* tau, float* work, hipStream_t s, float* Q = nullptr,
-                               void* img_q = nullptr, void* img_qt = nullptr);
+                               void* img_q = nullptr, void* img_qt = nullptr,
+                               unsigned* tcount = nullptr);
 size_t wide_quad_floats(int Dp, int64_t rows);
 hipError_t launch_wide_user_loss(int Dp, const LossArgs& a, hipStream_t s);
 hipError_t launch_user_loss(int Dp, const LossArgs& a, hipStream_t s);
@@ -293,6 +295,9 @@ hipError_t launch_zero_gram(int Dp, float* G, hipStream_t s);
 // Train-loss diagnostics: out[r] = ||X[r]||^2 for n rows; dot = sum_ij A_ij B_ij
 // (double, Dp x Dp).
 hipError_t launch_row_norm2(const float* X, int64_t n, int Dp, float* out, hipStream_t s);
+// ||X[r] - Y[r]||^2 per row (the print_residual_stats norms)
+hipError_t launch_row_diff2(const float* X, const float* Y, int64_t n, int Dp, float* out,
+                            hipStream_t s);
 hipError_t launch_gram_dot(const float* A, const float* B, int Dp, double* dot, hipStream_t s);
 
 // Padded leading dimension for a logical dimension (8, 16, multiples of 32
@@ -305,9 +310,5 @@ bool syrk_split_bf16();
 // (rows * Dp >= 2^32), or FRECSYS_GATHER64=1 forces them (tests: the two
 // widths are bit-identical).
 bool gather_off64(int64_t rows, int Dp);
-// Register-resident d-space solve at Dp = 256 (solve_rr.hip): two entities
-// per CU; the solve kinds only; opt-in with FRECSYS_RR=1.
-bool solve_rr_enabled(int Dp, int kind);
-hipError_t launch_solve_rr(const SolveArgs& a, hipStream_t s);
 
 }  // namespace frecsys_hip

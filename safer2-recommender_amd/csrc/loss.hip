@@ -247,15 +247,16 @@ hipError_t launch(const LossArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ||X[r]||^2, one wave per row.
-__global__ void __launch_bounds__(256) row_norm2_kernel(const float* __restrict__ X, int64_t n,
+// ||X[r] - Y[r]||^2 (Y may be null: ||X[r]||^2), one wave per row.
+__global__ void __launch_bounds__(256) row_norm2_kernel(const float* __restrict__ X,
+                                                        const float* __restrict__ Y, int64_t n,
                                                         int Dp, float* __restrict__ out) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= n) return;
   float s = 0.0f;
   for (int j = lane; j < Dp; j += 64) {
-    const float v = X[r * Dp + j];
+    const float v = Y ? X[r * Dp + j] - Y[r * Dp + j] : X[r * Dp + j];
     s += v * v;
   }
   s = wave_sum(s);
@@ -282,8 +283,16 @@ __global__ void __launch_bounds__(256) gram_dot_kernel(const float* __restrict__
 
 hipError_t launch_row_norm2(const float* X, int64_t n, int Dp, float* out, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(row_norm2_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, X, n, Dp,
-                     out);
+  hipLaunchKernelGGL(row_norm2_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, X,
+                     (const float*)nullptr, n, Dp, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_row_diff2(const float* X, const float* Y, int64_t n, int Dp, float* out,
+                            hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(row_norm2_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, X, Y, n,
+                     Dp, out);
   return hipGetLastError();
 }
 

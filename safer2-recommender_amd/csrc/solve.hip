@@ -941,7 +941,6 @@ hipError_t launch_solve(int Dp, const SolveArgs& a, hipStream_t s) {
     case 192: return launch_tiled<6, false>(a, s);
     case 224: return launch_tiled<7, false>(a, s);
     case 256:
-      if (solve_rr_enabled(Dp, a.kind)) return launch_solve_rr(a, s);
       return launch_tiled<8, false>(a, s);
     default: return hipErrorInvalidValue;
   }

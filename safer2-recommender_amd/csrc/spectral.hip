@@ -113,13 +113,14 @@ __device__ unsigned long long g_tri_prof[16][8];  // [wave][phase]
 __global__ void __launch_bounds__(512)
     tridiag_kernel(const float* __restrict__ G, int n, float* tdiag, float* toff, float* Vh,
                    float* tau_out, float* Q, bf16x8* img_q, bf16x8* img_qt,
-                   unsigned long long* vt, unsigned long long* tt) {
+                   unsigned long long* vt, unsigned long long* tt, unsigned* tcount) {
   typedef float f2 __attribute__((ext_vector_type(2)));  // v_pk_fma_f32 operands
   __shared__ __attribute__((aligned(16))) float vs[2][256];
   __shared__ __attribute__((aligned(16))) float ps[256];
   __shared__ float tsh[2];
   if (blockIdx.x > 0) {  // Q-row worker (reflectors k = 0 .. n-3)
-    qrows_worker<256, 512>(blockIdx.x - 1, n, n - 2, vt, tt, Q, img_q, img_qt, &vs[0][0], tsh);
+    qrows_worker<256, 512>(blockIdx.x - 1, n, n - 2, vt, tt, Q, img_q, img_qt, &vs[0][0], tsh,
+                           tcount);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63;
@@ -906,10 +907,10 @@ size_t tridiag_work_floats(int Dp) {
 
 hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
                           float* tau, hipStream_t s, float* work, float* Q, void* img_q,
-                          void* img_qt) {
+                          void* img_qt, unsigned* tcount) {
   if (Q && (!tridiag_forms_q(Dp) || !work)) return hipErrorInvalidValue;
   if ((img_q != nullptr) != (img_qt != nullptr) || (img_q && !Q)) return hipErrorInvalidValue;
-  if (wide_dim(Dp)) return launch_wide_tridiag(G, Dp, tdiag, toff, Vh, tau, work, s, Q, img_q, img_qt);
+  if (wide_dim(Dp)) return launch_wide_tridiag(G, Dp, tdiag, toff, Vh, tau, work, s, Q, img_q, img_qt, tcount);
   if (Dp < 4 || Dp > 256) return hipErrorInvalidValue;
   unsigned long long* vt = Q ? reinterpret_cast<unsigned long long*>(work) : nullptr;
   unsigned long long* tt = Q ? vt + (size_t)Dp * Dp : nullptr;
@@ -919,7 +920,8 @@ hipError_t launch_tridiag(const float* G, int Dp, float* tdiag, float* toff, flo
   }
   const unsigned grid = 1 + (Q ? (unsigned)(Dp / 32) : 0u);
   hipLaunchKernelGGL(tridiag_kernel, dim3(grid), dim3(512), 0, s, G, Dp, tdiag, toff, Vh, tau, Q,
-                     reinterpret_cast<bf16x8*>(img_q), reinterpret_cast<bf16x8*>(img_qt), vt, tt);
+                     reinterpret_cast<bf16x8*>(img_q), reinterpret_cast<bf16x8*>(img_qt), vt, tt,
+                     tcount);
   return hipGetLastError();
 }
 

@@ -58,7 +58,6 @@ namespace {
 
 constexpr int WB = 128;    // block-pair edge
 constexpr int WR = 16;     // rows per staged chunk
-constexpr int kWideMaxBlocks = 256;  // row blocks of the wide SYRK launches
 // Leaves of a wide Gramian (kernels.h GramPlan): 768 rather than 256, so that
 // a rank's two of the 16 groups at N = 8 still launch ~100 leaves x the block
 // pairs (the 1,842-row leaves of 256 took 376 us for the MSD user Gramian on
@@ -806,276 +805,6 @@ __global__ void __launch_bounds__(512)
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
-// Two panels per step (Dp = 512, opt-in with FRECSYS_WIDE_CHOL2=1): the same
-// factorisation as wide_chol_kernel<16>, bit for bit, with each streamed
-// L_Iq tile used for both panels p and p+1 -- half the workspace re-reads
-// (~T^3/12 tiles per entity instead of ~T^3/6).  Rows p and p+1 of L sit in
-// LDS (140 KB: one workgroup per CU).  Measured on the MSD bench: fabric
-// bytes 177.5 against 306.1 GB, but 7.64 against 5.24 ms per launch -- the
-// factor chain is latency-bound, and one workgroup per CU (and two
-// factorisations per step on wave 0's chain) cost more than the traffic
-// saved; so it is not the default.  Step (p, p+1):
-//   A  rows p, p+1 of L (q < p) into LDS;
-//   B  wave 0: L_pp^-1 (diag_factor_inv); wave 1: r_p, and C_{p+1,p} from
-//      the two LDS rows; waves 2..7: their first tile I, both sums
-//      C_Ip, C_I,p+1 over q < p from one stream of L_Iq;
-//   C  wave 0: y_p; wave 1: L_{p+1,p} into the workspace and LDS row p+1;
-//      waves 2..7: L_Ip = C_Ip^T L_pp^-T into the workspace;
-//   D  wave 0: L_{p+1,p+1}^-1; wave 1: r_{p+1}; waves 1..7: the q = p term
-//      of C_I,p+1 (L_Ip kept in registers) and their second tile;
-//   E  wave 0: y_{p+1}; waves 1..7: L_I,p+1 into the workspace.
-// The q = p term of panel p+1 reads L_Ip back from the tile the wave has
-// just stored (an L1/L2 hit), in the operand layout the one-panel kernel
-// streams it in, so every sum runs in the same order.  (Forming L_Ip
-// transposed by swapping the finish's MFMA operands instead, which skips
-// the read-back, differs in the last bit for about one element in a
-// thousand: the f32 MFMA is not bit-symmetric under that swap.)
-constexpr int WC2_T = 16;
-constexpr size_t wide_chol2_lds_floats() {
-  return (size_t)(2 * WC2_T - 1) * 33 * 32 + 1024 + 2 * 32 * WC2_T + 32 + 8 * 32 + 4;
-}
-
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
-    wide_chol2_kernel(SolveArgs a, int64_t pos0, float* ws) {
-  constexpr int T = WC2_T, Dp = 32 * T, NT = T * (T + 1) / 2, NW = 8, LP = 33 * 32;
-  typedef float f32x4v __attribute__((ext_vector_type(4)));
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* row0 = smem;                  // [T-2][LP] row p of L (q < p)
-  float* row1 = row0 + (T - 2) * LP;   // [T-1][LP] row p+1 of L (q <= p)
-  float* dpad0 = row1 + (T - 1) * LP;  // L_pp^-1
-  float* dpad1 = dpad0 + LP;           // L_{p+1,p+1}^-1
-  float* dinv = dpad1 + LP;            // swizzled factor tile
-  float* yv = dinv + 1024;
-  float* xv = yv + Dp;
-  float* rv = xv + Dp;
-  float* part = rv + 32;
-  int* flag = reinterpret_cast<int*>(part + NW * 32);
-  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const QueueRec rec = a.order[pos0 + blockIdx.x];
-  const int64_t e = rec.entity;
-  if (rec.h == 0) return;
-  float* slot = ws + (int64_t)blockIdx.x * ((int64_t)NT * 1024 + Dp);
-  auto gtile = [&](int I, int J) { return slot + (int64_t)tidx(I, J) * 1024; };
-  for (int i = tid; i < Dp; i += 512) yv[i] = slot[(int64_t)NT * 1024 + i];
-  if (tid == 0) flag[0] = 0;
-  __syncthreads();
-
-  // (A_IJ)^T in the accumulator layout (row lo, columns acc_row(q, hi))
-  auto load_c = [&](int I, int J) __attribute__((always_inline)) {
-    const float* Ap = gtile(I, J) + lo * 32 + 4 * hi;
-    f32x16 c;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4v v = *reinterpret_cast<const f32x4v*>(Ap + 8 * g);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) c[4 * g + j] = v[j];
-    }
-    return c;
-  };
-  // C_Ip and C_I,p+1 over q < p, L_Iq streamed once (next tile in flight)
-  auto dual_sum = [&](int I, int p, f32x16& c0, f32x16& c1) __attribute__((always_inline)) {
-    c0 = load_c(I, p);
-    c1 = load_c(I, p + 1);
-    f32x4v cur[4], nxt[4];
-    if (p > 0) {
-      const f32x4v* L0 = reinterpret_cast<const f32x4v*>(gtile(I, 0) + lo * 32 + 16 * hi);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = L0[j];
-    }
-#pragma unroll 1
-    for (int q = 0; q < p; ++q) {
-      if (q + 1 < p) {
-        const f32x4v* Ln = reinterpret_cast<const f32x4v*>(gtile(I, q + 1) + lo * 32 + 16 * hi);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) nxt[j] = Ln[j];
-      }
-      const float* P0 = row0 + q * LP + lo * 33 + 16 * hi;
-      const float* P1 = row1 + q * LP + lo * 33 + 16 * hi;
-#pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) {
-        c0 = mfma32(-P0[s2], cur[s2 >> 2][s2 & 3], c0);
-        c1 = mfma32(-P1[s2], cur[s2 >> 2][s2 & 3], c1);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
-    }
-  };
-  // L = C^T Linv^T as wide_chol_kernel forms it (lane (lo, hi) holds column
-  // lo, rows acc_row(q, hi)), stored row-major
-  auto finish = [&](const f32x16& c, const float* dp, float* tile) __attribute__((always_inline)) {
-    f32x16 l = f32x16{0.f};
-#pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2) l = mfma32(c[s2], dp[lo * 33 + acc_row(s2, hi)], l);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) tile[acc_row(q, hi) * 32 + lo] = l[q];
-    return l;
-  };
-  // the q = p term of panel p+1, c1 -= (L_Ip L_{p+1,p}^T)^T: L_Ip read back
-  // from the tile this wave just stored (the L1/L2 copy: the wave's stores
-  // complete first), in the operand order panel_sum streams it
-  auto fused = [&](f32x16& c1, const float* tile, int p) __attribute__((always_inline)) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const f32x4v* Lr = reinterpret_cast<const f32x4v*>(tile + lo * 32 + 16 * hi);
-    f32x4v r[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = Lr[j];
-    const float* P = row1 + p * LP + lo * 33 + 16 * hi;
-#pragma unroll
-    for (int s2 = 0; s2 < 16; ++s2) c1 = mfma32(-P[s2], r[s2 >> 2][s2 & 3], c1);
-  };
-  // wave 0: D = A_jj - sum_q L_jq L_jq^T from an LDS row, factored, inverted
-  auto diag = [&](int j, const float* rowb, int nq, float* dp) __attribute__((always_inline)) {
-    const float* Ajj = gtile(j, j);
-    f32x16 d;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) d[q] = Ajj[acc_row(q, hi) * 32 + lo];
-#pragma unroll 1
-    for (int q = 0; q < nq; ++q) {
-      const float* P = rowb + q * LP + lo * 33 + 16 * hi;
-#pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
-    }
-    int lo_o, hi_o;  // opaque lane coordinates (see wide_chol_kernel)
-    asm volatile("v_mov_b32 %0, %1" : "=v"(lo_o) : "v"(lo));
-    asm volatile("v_mov_b32 %0, %1" : "=v"(hi_o) : "v"(hi));
-#pragma unroll
-    for (int q = 0; q < 16; ++q) dinv[sw(acc_row(q, hi_o), lo_o)] = d[q];
-    wave_lds_sync();
-    if (!diag_factor_inv(dinv, lane) && lane == 0) flag[0] = 1;
-    wave_lds_sync();
-    float* Aw = gtile(j, j);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int r = 2 * i + hi_o;
-      const float v = dinv[sw(r, lo_o)];
-      Aw[r * 32 + lo_o] = v;
-      dp[r * 33 + lo_o] = v;
-    }
-  };
-  auto resid = [&](int j, const float* rowb, int nq) __attribute__((always_inline)) {
-    float r = 0.0f;
-#pragma unroll 1
-    for (int q = 0; q < nq; ++q) {
-      const float* L = rowb + q * LP + lo * 33 + 16 * hi;
-      const float* y = yv + 32 * q + 16 * hi;
-#pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) r = __builtin_fmaf(L[k2], y[k2], r);
-    }
-    r += __shfl_xor(r, 32);
-    if (hi == 0) rv[lo] = yv[32 * j + lo] - r;
-  };
-  auto ysolve = [&](int j, const float* dp) __attribute__((always_inline)) {
-    float y = 0.0f;
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) y = __builtin_fmaf(dp[lo * 33 + 16 * hi + k2], rv[16 * hi + k2], y);
-    y += __shfl_xor(y, 32);
-    if (hi == 0) yv[32 * j + lo] = y;
-  };
-
-#pragma unroll 1
-  for (int p = 0; p < T; p += 2) {
-    // ---- A: rows p and p+1 of L, q < p (loads issued seven at a time) ----
-    {
-      constexpr int NA = (2 * (T - 2) * 256 + 511) / 512, NB = 7;
-      const int n = p * 256, n2 = 2 * n;
-#pragma unroll
-      for (int k0 = 0; k0 < NA; k0 += NB) {
-        if (tid + 512 * k0 < n2) {  // wave-uniform (n2 is a multiple of 512)
-          float4 v[NB];
-#pragma unroll
-          for (int k = 0; k < NB; ++k) {
-            const int i = tid + 512 * (k0 + k);
-            const int ii = i < n2 ? i : tid;
-            const int rr = ii >= n ? 1 : 0, jj = ii - rr * n;
-            const int q = jj >> 8, r = (jj >> 3) & 31, c = (jj & 7) * 4;
-            v[k] = *reinterpret_cast<const float4*>(gtile(p + rr, q) + r * 32 + c);
-          }
-#pragma unroll
-          for (int k = 0; k < NB; ++k) {
-            const int i = tid + 512 * (k0 + k);
-            if (i < n2) {
-              const int rr = i >= n ? 1 : 0, jj = i - rr * n;
-              const int q = jj >> 8, r = (jj >> 3) & 31, c = (jj & 7) * 4;
-              float* t = (rr ? row1 : row0) + q * LP + r * 33 + c;
-              t[0] = v[k].x;
-              t[1] = v[k].y;
-              t[2] = v[k].z;
-              t[3] = v[k].w;
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // wave w >= 1 owns tiles Ia = p+1+w and Ib = p+8+w (of p+2 .. T-1)
-    const int Ia = p + 1 + wave, Ib = p + 8 + wave;
-    f32x16 c0a, c1a, c1b;
-    // ---- B ----
-    if (wave == 0) {
-      diag(p, row0, p, dpad0);
-    } else if (wave == 1) {
-      resid(p, row0, p);
-      // C_{p+1,p}: L_{p+1,q} from LDS row p+1 (the same values the
-      // workspace holds), in the order of panel_sum
-      c0a = load_c(p + 1, p);
-#pragma unroll 1
-      for (int q = 0; q < p; ++q) {
-        const float* P0 = row0 + q * LP + lo * 33 + 16 * hi;
-        const float* P1 = row1 + q * LP + lo * 33 + 16 * hi;
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) c0a = mfma32(-P0[s2], P1[s2], c0a);
-      }
-    } else if (Ia < T) {
-      dual_sum(Ia, p, c0a, c1a);
-    }
-    __syncthreads();
-    // ---- C ----
-    if (wave == 0) {
-      ysolve(p, dpad0);
-    } else if (wave == 1) {
-      const f32x16 l = finish(c0a, dpad0, gtile(p + 1, p));
-      float* Lr = row1 + p * LP + lo;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) Lr[acc_row(q, hi) * 33] = l[q];
-    } else if (Ia < T) {
-      finish(c0a, dpad0, gtile(Ia, p));
-    }
-    __syncthreads();
-    // ---- D ----
-    if (wave == 0) {
-      diag(p + 1, row1, p + 1, dpad1);
-    } else {
-      if (wave == 1) {
-        resid(p + 1, row1, p + 1);
-        if (Ia < T) {
-          dual_sum(Ia, p, c0a, c1a);
-          finish(c0a, dpad0, gtile(Ia, p));
-        }
-      }
-      if (Ia < T) fused(c1a, gtile(Ia, p), p);
-      if (Ib < T) {
-        f32x16 c0b;
-        dual_sum(Ib, p, c0b, c1b);
-        finish(c0b, dpad0, gtile(Ib, p));
-        fused(c1b, gtile(Ib, p), p);
-      }
-    }
-    __syncthreads();
-    // ---- E ----
-    if (wave == 0) {
-      ysolve(p + 1, dpad1);
-    } else {
-      if (Ia < T) finish(c1a, dpad1, gtile(Ia, p + 1));
-      if (Ib < T) finish(c1b, dpad1, gtile(Ib, p + 1));
-    }
-    __syncthreads();
-  }
-  wide_back_subst<T>(slot, yv, xv, part, wave, lo, hi);
-  for (int i = tid; i < Dp; i += 512) a.out[e * Dp + i] = xv[i];
-  if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
-}
-
 // CVaR-MF: x = e - eta (A_full e - b), A_full's strict upper part the stale
 // G part (cvar_upper); one workgroup per entity.
 __global__ void __launch_bounds__(256)
@@ -1434,7 +1163,7 @@ __global__ void __launch_bounds__(256)
                           int* err, float* __restrict__ Vh, float* __restrict__ tau,
                           float* __restrict__ tdiag, float* __restrict__ toff, float* Q,
                           bf16x8* img_q, bf16x8* img_qt, unsigned long long* vt,
-                          unsigned long long* tt) {
+                          unsigned long long* tt, unsigned* tcount) {
   constexpr int n = N, CW = 16, NR = N / 16, NV = N / 256, NWG = N / CW;
   __shared__ float lbuf[3 * N];
   float* vp = lbuf;
@@ -1444,7 +1173,7 @@ __global__ void __launch_bounds__(256)
   __shared__ float pc[16][CW + 1];
   __shared__ float tsh;
   if (blockIdx.x >= NWG) {  // Q-row worker (reflectors k = 0 .. n-2)
-    qrows_worker<N, 256>(blockIdx.x - NWG, n, n - 1, vt, tt, Q, img_q, img_qt, lbuf, red);
+    qrows_worker<N, 256>(blockIdx.x - NWG, n, n - 1, vt, tt, Q, img_q, img_qt, lbuf, red, tcount);
     return;
   }
   const int c0 = blockIdx.x * CW;
@@ -1467,8 +1196,8 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int r = tid + 256 * j;
-      pir[j] = (k > 0 && r >= k) ? tpoll(pin + r, tin, err) : 0.0f;
-      akr[j] = r >= k ? (k == 0 ? G[r] : tpoll(pin + N + r, tin, err)) : 0.0f;
+      pir[j] = (k > 0 && r >= k) ? tpoll(pin + r, tin, err, false, tcount) : 0.0f;
+      akr[j] = r >= k ? (k == 0 ? G[r] : tpoll(pin + N + r, tin, err, false, tcount)) : 0.0f;
     }
     float d = 0.0f;
     if (tp != 0.0f) {
@@ -1618,12 +1347,6 @@ __global__ void __launch_bounds__(256) loss_gather_wide_kernel(LossArgs a) {
   if (lane == 0) a.out[e] = loss;
 }
 
-int64_t wide_rows_per_block(int64_t n) {
-  int64_t rpb = (n + kWideMaxBlocks - 1) / kWideMaxBlocks;
-  if (rpb < 256) rpb = 256;
-  return (rpb + WR - 1) / WR * WR;
-}
-
 unsigned xcd_grid(int64_t n_units, int P) { return (unsigned)(((n_units + 7) / 8) * 8 * P); }
 
 size_t wide_chol_lds_bytes(int Dp) {
@@ -1689,17 +1412,9 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
       err = hipFuncSetAttribute((const void*)wide_chol_kernel<32>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(1024));
-    if (err == hipSuccess)
-      err = hipFuncSetAttribute((const void*)wide_chol2_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(float) * wide_chol2_lds_floats()));
     if (err != hipSuccess) return err;
     attr = true;
   }
-  // FRECSYS_WIDE_CHOL2=1: two panels per step (opt-in, measured slower;
-  // read at each call)
-  const char* c2 = getenv("FRECSYS_WIDE_CHOL2");
-  const bool two_panels = c2 && c2[0] == '1';
   const bool grad = is_grad_kind(a.kind);
   GramArgs g{};
   // the slabs of the long histories (all in the first batch) first
@@ -1722,9 +1437,6 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
-    else if (Dp == 512 && two_panels)
-      hipLaunchKernelGGL(wide_chol2_kernel, dim3((unsigned)nb), dim3(512),
-                         sizeof(float) * wide_chol2_lds_floats(), s, a, s0, ws);
     else if (Dp == 512)
       hipLaunchKernelGGL(wide_chol_kernel<16>, dim3((unsigned)nb), dim3(512),
                          wide_chol_lds_bytes(Dp), s, a, s0, ws);
@@ -1757,7 +1469,7 @@ bool tridiag_steps() {
 
 hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,
                                float* tau, float* work, hipStream_t s, float* Q, void* img_q,
-                               void* img_qt) {
+                               void* img_qt, unsigned* tcount) {
   if (!wide_dim(Dp) || !work) return hipErrorInvalidValue;
   if (!tridiag_steps()) {
     float* xbuf = work;                                     // [2][2][Dp]
@@ -1781,10 +1493,10 @@ hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff
       bf16x8* iqt = reinterpret_cast<bf16x8*>(img_qt);
       if (Dp == 512)
         hipLaunchKernelGGL(tridiag_tagged_kernel<512>, dim3(grid), dim3(256), 0, s, G, xb, 0u, err,
-                           Vh, tau, tdiag, toff, Q, iq, iqt, vt, tt);
+                           Vh, tau, tdiag, toff, Q, iq, iqt, vt, tt, tcount);
       else
         hipLaunchKernelGGL(tridiag_tagged_kernel<1024>, dim3(grid), dim3(256), 0, s, G, xb, 0u,
-                           err, Vh, tau, tdiag, toff, Q, iq, iqt, vt, tt);
+                           err, Vh, tau, tdiag, toff, Q, iq, iqt, vt, tt, tcount);
       return hipGetLastError();
     }
     if (Dp == 512)

@@ -39,7 +39,7 @@ EXPORTS = (
     "frecsys_pp_predict", "frecsys_pp_step", "frecsys_debug_diag_factor",
     "frecsys_history_space_max_h", "frecsys_comm_world", "frecsys_gram_groups",
     "frecsys_get_gram_groups", "frecsys_set_gram_groups", "frecsys_get_gramian",
-    "frecsys_gram_plan", "frecsys_work",
+    "frecsys_gram_plan", "frecsys_work", "frecsys_snapshot_residual", "frecsys_counter",
 )
 
 # Every symbol include/frecsys_model.h declares.
@@ -138,6 +138,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_pp_set_rating_index": (ctypes.c_int, [P, I32, P]),
         "frecsys_pp_predict": (ctypes.c_int, [P, I32]),
         "frecsys_pp_step": (ctypes.c_int, [P, I32, I32, I32, P, P]),
+        "frecsys_snapshot_residual": (ctypes.c_int, [P, I32, P]),
+        "frecsys_counter": (ctypes.c_int, [P, ctypes.c_char_p, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -330,6 +332,18 @@ class Context:
 
     def snapshot(self, side: int):
         self._check(self.lib.frecsys_snapshot(self.h, side))
+
+    def snapshot_residual(self, side: int) -> float:
+        """sum over rows of ||X_r - snapshot_r||^2 (double, on the device)."""
+        sq = ctypes.c_double()
+        self._check(self.lib.frecsys_snapshot_residual(self.h, side, ctypes.byref(sq)))
+        return float(sq.value)
+
+    def counter(self, what: str) -> int:
+        """Cumulative event counter: "hspace_reruns" or "tagged_timeouts"."""
+        v = ctypes.c_int64()
+        self._check(self.lib.frecsys_counter(self.h, what.encode(), ctypes.byref(v)))
+        return int(v.value)
 
     # -- compute --
     def gramian(self, side: int, weights: Optional[np.ndarray] = None,

@@ -56,8 +56,15 @@ class CVaRMFRecommender : public detail::DeviceModel {
     dev_->LoadTraining(data);
     PrintWeightedLosses(data, regularization_, unobserved_weight_, alpha_);  // cvar_mf.h:277
     const Csr& uc = data.user_csr();
+    VectorXf w_prev;
+    if (print_residualstats_) w_prev = dual_weight_;
     for (int64_t u = 0; u < uc.rows() && u < num_users_; ++u)  // cvar_mf.h:597-642
       if (uc.len(u)) dual_weight_[u] = (float)((user_loss_[u] - prev_xi_) >= 0);
+    // residual norms (print_residual_stats): z = (omega - omega_prev).norm()
+    // (cvar_mf.h:637-640); StepU returns 0 (cvar_mf.h:472-473); V against
+    // its pre-step value (cvar_mf.h:533-536), on the device from a snapshot
+    const float residual_z = print_residualstats_ ? WeightResidual(dual_weight_, w_prev) : 0.0f;
+    const float residual_U = 0.0f;
     dev_->Snapshot(DeviceContext::USER);  // user_embedding_prev, cvar_mf.h:282
     frecsys_solve_params pu = solve_params(FRECSYS_KIND_CVAR_GRAD_U, regularization_,
                                            unobserved_weight_);
@@ -74,7 +81,9 @@ class CVaRMFRecommender : public detail::DeviceModel {
     pv.from_snapshot = 1;
     pv.entity_reg = item_reg_.data();
     pv.other_weight = nu.data();
+    if (print_residualstats_) dev_->Snapshot(DeviceContext::ITEM);
     dev_->Solve(DeviceContext::ITEM, pv);  // cvar_mf.h:293-295
+    const float residual_V = print_residualstats_ ? dev_->SnapshotResidual(DeviceContext::ITEM) : 0.0f;
     dev_->Gramian(DeviceContext::ITEM);    // cvar_mf.h:297-298
     dev_->UserLoss(DeviceContext::USER, unobserved_weight_, true, user_loss_.data());
     VectorXf wl(num_users_);
@@ -86,6 +95,9 @@ class CVaRMFRecommender : public detail::DeviceModel {
       LOG(INFO) << format("Min: {0:.3f}, Mean: {1:.3f}, Max: {2:.3f}", dual_weight_.minCoeff(),
                           dual_weight_.mean(), dual_weight_.maxCoeff());
     }
+    if (print_residualstats_)  // cvar_mf.h:322-326
+      LOG(INFO) << format("U residual: {0}, V residual: {1}, z residual: {2}", residual_U,
+                          residual_V, residual_z);
     const float xi = ComputeXi(user_loss_);
     LOG(INFO) << "Xi:" << xi;
     prev_xi_ = xi;

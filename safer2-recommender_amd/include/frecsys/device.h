@@ -10,6 +10,7 @@
 #pragma once
 
 #include <array>
+#include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -111,6 +112,13 @@ class DeviceContext {
     bump(side);
   }
   void Snapshot(int side) { check(frecsys_snapshot(ctx_, side), "snapshot"); }
+  // ||X - snapshot|| over every row of side (the residual norms of
+  // --print_residual_stats), on the device; sqrt of a double sum.
+  float SnapshotResidual(int side) {
+    double sq = 0.0;
+    check(frecsys_snapshot_residual(ctx_, side, &sq), "snapshot_residual");
+    return (float)std::sqrt(sq);
+  }
 
   // ---- Gramians: slot `side` holds G of side's embeddings, optionally
   //      weighted; recomputed only when the embeddings or weights changed.

@@ -63,7 +63,11 @@ class ERMMFRecommender : public detail::DeviceModel {
     frecsys_solve_params pu = solve_params(FRECSYS_KIND_WEIGHTED_U, regularization_,
                                            unobserved_weight_);
     pu.entity_weight = dual_weight_.data();
+    // residual norms (print_residual_stats, erm_mf.h:434-448, 508-512): U
+    // and V against their pre-step values, on the device from snapshots
+    if (print_residualstats_) dev_->Snapshot(DeviceContext::USER);
     dev_->Solve(DeviceContext::USER, pu);  // erm_mf.h:259-267
+    const float residual_U = print_residualstats_ ? dev_->SnapshotResidual(DeviceContext::USER) : 0.0f;
     std::vector<float> nu((size_t)num_users_);
     for (int64_t u = 0; u < num_users_; ++u) nu[u] = dual_weight_[u] / user_history_size_[u];
     dev_->Gramian(DeviceContext::USER, dual_weight_.data(), ++weight_epoch_);
@@ -72,7 +76,9 @@ class ERMMFRecommender : public detail::DeviceModel {
     pv.alpha = alpha_;
     pv.entity_reg = item_reg_.data();
     pv.other_weight = nu.data();
+    if (print_residualstats_) dev_->Snapshot(DeviceContext::ITEM);
     dev_->Solve(DeviceContext::ITEM, pv);  // erm_mf.h:269-271
+    const float residual_V = print_residualstats_ ? dev_->SnapshotResidual(DeviceContext::ITEM) : 0.0f;
     dev_->Gramian(DeviceContext::ITEM);    // erm_mf.h:273-274
     dev_->UserLoss(DeviceContext::USER, unobserved_weight_, true, user_loss_.data());
     VectorXf wl(num_users_);
@@ -83,8 +89,8 @@ class ERMMFRecommender : public detail::DeviceModel {
       LOG(INFO) << format("Min: {0:.3f}, Mean: {1:.3f}, Max: {2:.3f}", dual_weight_.minCoeff(),
                           dual_weight_.mean(), dual_weight_.maxCoeff());
     }
-    if (print_residualstats_)
-      LOG(INFO) << format("U residual: {0}, V residual: {1}", 0.0f, 0.0f);
+    if (print_residualstats_)  // erm_mf.h:297-300
+      LOG(INFO) << format("U residual: {0}, V residual: {1}", residual_U, residual_V);
   }
 
   // Initialize (erm_mf.h:573-587).

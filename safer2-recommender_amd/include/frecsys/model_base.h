@@ -175,6 +175,17 @@ class DeviceModel : public Recommender {
     LOG(INFO) << format("Time={0}", (int64_t)ms);
   }
 
+  // (w - w_prev).norm() of the dual weights (ComputeUserWeights' residual,
+  // safer2.h:789-792, cvar_mf.h:637-640), in double.
+  static float WeightResidual(const VectorXf& w, const VectorXf& prev) {
+    double s = 0.0;
+    for (int64_t i = 0; i < w.size(); ++i) {
+      const double d = (double)w[i] - (double)prev[i];
+      s += d * d;
+    }
+    return (float)std::sqrt(s);
+  }
+
   static double RowSqNorm(const MatrixXf& M, int64_t r) {
     double s = 0;
     for (int64_t j = 0; j < M.cols(); ++j) s += (double)M(r, j) * M(r, j);

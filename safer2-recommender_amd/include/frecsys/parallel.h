@@ -44,47 +44,56 @@ class ThreadPool {
 
   // fn(lo, hi) over [0, n) in contiguous ranges; the caller runs one range.
   // Small n runs inline, and so does a call made while the pool serves
-  // another caller (models trained from two host threads, or a nested call):
-  // the pool holds one job at a time, and the per-index results do not
-  // depend on the split.
+  // another caller (models trained from two host threads, or a nested call
+  // from inside a task): the pool holds one job at a time, and the per-index
+  // results do not depend on the split.
   //
   // The smoothed-quantile Newton issues ~12 jobs of ~30 us each back to
   // back per epoch; a condition-variable hand-off per job (futex wake of
   // every worker, then a futex wait for the last one) cost more than the
   // work.  So the hand-off is lock-free: workers spin on the job generation
   // for up to kSpinUs after their last task before they sleep, and the
-  // caller spins on the pending count.
+  // caller spins until the job is drained.
+  //
+  // Job lifetime.  gen_ is odd while a job is open, even between jobs.  The
+  // caller writes the job (job_, n_, tasks_, next_), opens it (gen_ odd),
+  // runs tasks until none is left, closes it (gen_ even) and then waits for
+  // active_ == 0.  A worker that saw open generation g joins it by
+  // incrementing active_ and only then re-reads gen_: if g is no longer open
+  // it backs off without touching the job.  The two seq_cst pairs
+  // (worker: active_++ then gen_ load; caller: gen_++ then active_ load)
+  // guarantee that either the worker sees the job closed or the caller sees
+  // the worker counted, so a job's fields are never rewritten while a worker
+  // that joined it still reads them.
   void ParallelFor(int64_t n, int64_t min_per_task,
                    const std::function<void(int64_t, int64_t)>& fn) {
     const int64_t tasks =
         std::max<int64_t>(1, std::min<int64_t>(size(), n / std::max<int64_t>(1, min_per_task)));
-    std::unique_lock<std::mutex> owner(call_mu_, std::try_to_lock);
-    if (tasks <= 1 || workers_.empty() || !owner.owns_lock()) {
+    bool idle = false;
+    if (tasks <= 1 || workers_.empty() ||
+        !busy_.compare_exchange_strong(idle, true, std::memory_order_acquire,
+                                       std::memory_order_relaxed)) {
       if (n > 0) fn(0, n);
       return;
     }
     job_ = &fn;
     n_ = n;
     tasks_ = tasks;
-    pending_.store(tasks - 1, std::memory_order_relaxed);
     next_.store(1, std::memory_order_relaxed);
-    gen_.fetch_add(1, std::memory_order_release);
-    if (sleepers_.load(std::memory_order_acquire) > 0) {
+    gen_.fetch_add(1, std::memory_order_seq_cst);  // open (odd)
+    if (sleepers_.load(std::memory_order_seq_cst) > 0) {
       std::lock_guard<std::mutex> lk(mu_);
       cv_.notify_all();
     }
     fn(0, n / tasks);  // task 0 on the caller
     // then any task no worker has taken yet
-    for (int64_t t; (t = next_.fetch_add(1, std::memory_order_acq_rel)) < tasks;) {
+    for (int64_t t; (t = next_.fetch_add(1, std::memory_order_relaxed)) < tasks;)
       fn(n * t / tasks, n * (t + 1) / tasks);
-      pending_.fetch_sub(1, std::memory_order_acq_rel);
-    }
-    // every task done and every worker out of this job's task loop (so none
-    // touches next_ once the next job has reset it)
-    while (pending_.load(std::memory_order_acquire) > 0 ||
-           active_.load(std::memory_order_acquire) > 0)
-      Relax();
+    gen_.fetch_add(1, std::memory_order_seq_cst);  // close (even): no new worker joins
+    // every worker that joined has finished its tasks and left the job
+    while (active_.load(std::memory_order_seq_cst) > 0) Relax();
     job_ = nullptr;
+    busy_.store(false, std::memory_order_release);
   }
 
   ~ThreadPool() {
@@ -109,46 +118,51 @@ class ThreadPool {
     for (int i = 1; i < n; ++i) workers_.emplace_back([this] { Loop(); });
   }
 
+  // an open job this worker has not joined yet
+  static bool Joinable(uint64_t g, uint64_t seen) { return (g & 1) && g != seen; }
+
   void Loop() {
-    uint64_t seen = gen_.load(std::memory_order_acquire);
+    uint64_t seen = 0;
     for (;;) {
       // wait for a new job: spin, then sleep
       auto t0 = std::chrono::steady_clock::now();
       int spins = 0;
       uint64_t g;
-      while ((g = gen_.load(std::memory_order_acquire)) == seen) {
+      while (!Joinable(g = gen_.load(std::memory_order_acquire), seen)) {
         if (stop_.load(std::memory_order_acquire)) return;
         Relax();
         if ((++spins & 255) == 0 &&
             std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) {
           std::unique_lock<std::mutex> lk(mu_);
-          sleepers_.fetch_add(1, std::memory_order_acq_rel);
+          sleepers_.fetch_add(1, std::memory_order_seq_cst);
           cv_.wait(lk, [&] {
             return stop_.load(std::memory_order_acquire) ||
-                   gen_.load(std::memory_order_acquire) != seen;
+                   Joinable(gen_.load(std::memory_order_seq_cst), seen);
           });
-          sleepers_.fetch_sub(1, std::memory_order_acq_rel);
+          sleepers_.fetch_sub(1, std::memory_order_relaxed);
           t0 = std::chrono::steady_clock::now();
         }
       }
       seen = g;
-      active_.fetch_add(1, std::memory_order_acq_rel);
-      for (int64_t t; (t = next_.fetch_add(1, std::memory_order_acq_rel)) < tasks_;) {
-        (*job_)(n_ * t / tasks_, n_ * (t + 1) / tasks_);
-        pending_.fetch_sub(1, std::memory_order_acq_rel);
+      active_.fetch_add(1, std::memory_order_seq_cst);
+      if (gen_.load(std::memory_order_seq_cst) == g) {  // still open: joined
+        const std::function<void(int64_t, int64_t)>& job = *job_;
+        const int64_t n = n_, tasks = tasks_;
+        for (int64_t t; (t = next_.fetch_add(1, std::memory_order_relaxed)) < tasks;)
+          job(n * t / tasks, n * (t + 1) / tasks);
       }
-      active_.fetch_sub(1, std::memory_order_acq_rel);
+      active_.fetch_sub(1, std::memory_order_release);
     }
   }
 
   std::vector<std::thread> workers_;
-  std::mutex call_mu_;  // held by the caller whose job the pool runs
-  std::mutex mu_;       // sleeping workers only
+  std::atomic<bool> busy_{false};  // a caller's job owns the pool
+  std::mutex mu_;                  // sleeping workers only
   std::condition_variable cv_;
   const std::function<void(int64_t, int64_t)>* job_ = nullptr;
   int64_t n_ = 0, tasks_ = 0;
   std::atomic<uint64_t> gen_{0};
-  std::atomic<int64_t> next_{0}, pending_{0};
+  std::atomic<int64_t> next_{0};
   std::atomic<int> active_{0}, sleepers_{0};
   std::atomic<bool> stop_{false};
 };

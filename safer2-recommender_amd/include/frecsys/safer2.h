@@ -219,12 +219,22 @@ class SAFER2Recommender : public detail::DeviceModel {
     double tw = 0, tu = 0, tv = 0, tl = 0;
     for (int t = 0; t < pd_iterations_; ++t) {
       auto a = now();
+      // residual norms (print_residual_stats): omega, U and V against their
+      // values before this iteration's updates (safer2.h:475-489, 550-554,
+      // 789-793), computed on the device from snapshots
+      VectorXf w_prev;
+      if (print_residualstats_) w_prev = dual_weight_;
       ComputeUserWeights(data);                                   // safer2.h:272-273
+      const float residual_z = print_residualstats_ ? WeightResidual(dual_weight_, w_prev) : 0.0f;
       auto b = now();
       frecsys_solve_params pu = u_params(true);
+      if (print_residualstats_) dev_->Snapshot(DeviceContext::USER);
       dev_->Solve(DeviceContext::USER, pu);                       // safer2.h:277-285
+      const float residual_U = print_residualstats_ ? dev_->SnapshotResidual(DeviceContext::USER) : 0.0f;
       auto c = now();
+      if (print_residualstats_) dev_->Snapshot(DeviceContext::ITEM);
       StepV(data);                                                // safer2.h:288-290
+      const float residual_V = print_residualstats_ ? dev_->SnapshotResidual(DeviceContext::ITEM) : 0.0f;
       auto d = now();
       dev_->Gramian(DeviceContext::ITEM);                         // safer2.h:294-295
       dev_->UserLoss(DeviceContext::USER, unobserved_weight_, true, user_loss_.data());
@@ -242,8 +252,9 @@ class SAFER2Recommender : public detail::DeviceModel {
         LOG(INFO) << format("Min: {0:.3f}, Mean: {1:.3f}, Max: {2:.3f}", dual_weight_.minCoeff(),
                             dual_weight_.mean(), dual_weight_.maxCoeff());
       }
-      if (print_residualstats_)
-        LOG(INFO) << format("U residual: {0}, V residual: {1}, z residual: {2}", 0.0f, 0.0f, 0.0f);
+      if (print_residualstats_)  // safer2.h:323-328
+        LOG(INFO) << format("U residual: {0}, V residual: {1}, z residual: {2}", residual_U,
+                            residual_V, residual_z);
     }
     auto x0 = now();
     const float xi = ComputeXi(user_loss_, prev_xi_, xi_iterations_);  // safer2.h:331-333

@@ -41,7 +41,10 @@ int main(int argc, char** argv) {
   frecsys::ERMMFRecommender* erm = nullptr;
   frecsys::CVaRMFRecommender* cv = nullptr;
   if (model == "ials") {
-    m = new frecsys::IALSRecommender(dim, nu, ni, reg, 1.0f, w, 0.1f, alpha, false, 1e-10, 100, o);
+    // MODEL_DUMP_REG_EXP: iALS l2_reg_exp (default 1, run_model.cc:143-145)
+    const char* re = getenv("MODEL_DUMP_REG_EXP");
+    m = new frecsys::IALSRecommender(dim, nu, ni, reg, re ? (float)atof(re) : 1.0f, w, 0.1f, alpha,
+                                     false, 1e-10, 100, o);
   } else if (model == "safer2") {
     s2 = new frecsys::SAFER2Recommender(dim, nu, ni, reg, w, bw, alpha, 0.1f, 5, 1, epan, use_snr,
                                         sampling_ratio, false, 1e-10, 100, o);
@@ -56,6 +59,9 @@ int main(int argc, char** argv) {
     return 3;
   }
   m->SetPrintTrainStats(false);
+  // MODEL_DUMP_RESIDUAL_STATS=1: --print_residual_stats (the residual-norm
+  // log lines, tests/test_models_gpu.py::test_residual_stats_match_oracle)
+  if (const char* rs = getenv("MODEL_DUMP_RESIDUAL_STATS")) m->SetPrintResidualStats(atoi(rs) != 0);
   if (s2) s2->Initialize(train);
   if (erm) erm->Initialize(train);
   if (cv) cv->Initialize(train);

@@ -82,7 +82,10 @@ def c5():
     V1 = ctx.get_embeddings(fh.SIDE_ITEM)
     GU1 = ctx.get_gramian(fh.SIDE_USER)  # U1^T diag(omega) U1 of the V step
     omega, loss, item_reg, xi = m.dual_state()
+    # the silent slow path never taken (frecsys_counter)
+    reruns, timeouts = ctx.counter("hspace_reruns"), ctx.counter("tagged_timeouts")
     m.close()
+    assert (reruns, timeouts) == (0, 0)
     _progress("fixture done")
     return dict(up=up, uc=uc, ip=ip, ic=ic, U0=U0, V0=V0, GV0=GV0, U1=U1, V1=V1, GU1=GU1,
                 omega=omega, loss=loss, item_reg=item_reg, xi=xi, epoch_s=epoch_s)

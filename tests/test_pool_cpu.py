@@ -17,6 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = r"""
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 #include "frecsys/parallel.h"
@@ -30,9 +31,16 @@ static int check_once(int64_t n, int64_t min_per_task) {
     if (hit[(size_t)i] != 1) return 1;
   return 0;
 }
-int main() {
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 2000;
   int bad = 0;
-  for (int rep = 0; rep < 2000; ++rep) bad += check_once(1 + (rep * 7919) % 20000, 64 + rep % 512);
+  for (int rep = 0; rep < reps; ++rep) bad += check_once(1 + (rep * 7919) % 20000, 64 + rep % 512);
+  // a small-task job right after a large one (a late worker of the large job
+  // must never run a task of the small one with the large one's fields)
+  for (int rep = 0; rep < reps; ++rep) {
+    bad += check_once(200000, 1);
+    bad += check_once(8 + rep % 5, 1);
+  }
   // two callers at once: one gets the pool, the other runs inline
   std::atomic<int> bad2{0};
   auto worker = [&] {
@@ -52,17 +60,45 @@ int main() {
 """
 
 
-@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ missing")
-def test_pool_visits_every_index_once(tmp_path):
+def _build_run(tmp_path, flags, reps):
     src = tmp_path / "pool.cc"
     src.write_text(SRC)
     exe = tmp_path / "pool"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-I",
+    subprocess.run(["g++", "-O2", "-g", "-std=c++17", "-pthread", *flags, "-I",
                     os.path.join(ROOT, "safer2-recommender_amd", "include"), "-o", str(exe),
                     str(src)], check=True)
-    env = dict(os.environ, OMP_NUM_THREADS="4")
-    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True, timeout=120,
-                         env=env).stdout.split()
+    env = dict(os.environ, OMP_NUM_THREADS="4", TSAN_OPTIONS="halt_on_error=1 exitcode=66")
+    r = subprocess.run([str(exe), str(reps)], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "WARNING: ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+    return r.stdout.split()
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ missing")
+def test_pool_visits_every_index_once(tmp_path):
+    out = _build_run(tmp_path, [], 2000)
+    bad, bad2, total, size = map(int, out)
+    assert bad == 0 and bad2 == 0
+    assert total == 4096
+    assert size == 4
+
+
+def _tsan_available(tmp_path):
+    probe = tmp_path / "probe.cc"
+    probe.write_text("int main() { return 0; }\n")
+    r = subprocess.run(["g++", "-fsanitize=thread", "-o", str(tmp_path / "probe"), str(probe)],
+                       capture_output=True)
+    return r.returncode == 0 and subprocess.run([str(tmp_path / "probe")]).returncode == 0
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ missing")
+def test_pool_thread_sanitizer_clean(tmp_path):
+    """The same program under ThreadSanitizer (host code only): no data race
+    in the job hand-off (the publication of job_ / n_ / tasks_ to workers)."""
+    if not _tsan_available(tmp_path):
+        pytest.skip("ThreadSanitizer runtime unavailable")
+    out = _build_run(tmp_path, ["-fsanitize=thread"], 200)
     bad, bad2, total, size = map(int, out)
     assert bad == 0 and bad2 == 0
     assert total == 4096

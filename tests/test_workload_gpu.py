@@ -56,6 +56,13 @@ def _check(name, got, ref, rows, ptr, **kw):
     assert e.max() < TOL_ROW, (name, float(e.max()), int(h[int(np.argmax(e))]))
 
 
+def _no_slow_path(ctx):
+    """No history-space side reran in d-space and no tagged poll timed out
+    (frecsys_counter): the benchmark data never takes the silent slow path."""
+    assert ctx.counter("hspace_reruns") == 0
+    assert ctx.counter("tagged_timeouts") == 0
+
+
 @pytest.fixture(scope="module")
 def ml20m():
     return synthetic(SHAPES["ml20m"])
@@ -95,6 +102,7 @@ def test_ials_ml20m_d256_half_steps(ml20m):
     Vo, rc = O.step(rp, cl, Ug, O.gramian(Ug), 0, reg, w, out=V0[rows].copy())
     assert rc == 0
     _check("ials_ml20m_d256_item", Vg, Vo, rows, ip)
+    _no_slow_path(ctx)
     ctx.close()
 
 
@@ -120,6 +128,7 @@ def test_safer2_ml20m_d256_train_epoch(ml20m, use_snr):
     U, V = ctx.get_embeddings(fh.SIDE_USER), ctx.get_embeddings(fh.SIDE_ITEM)
     mw = m.mean_weight()
     w_gpu, l_gpu, _, xi_gpu = m.dual_state()
+    _no_slow_path(ctx)
     m.close()
     om = O.Model(O.MODEL_SAFER2, d, nu, ni, reg=flags["l2_reg"], w=flags["uobs_weight"],
                  alpha=flags["alpha"], bandwidth=flags["bandwidth"], xi_iterations=5,
@@ -169,6 +178,7 @@ def test_ials_msd_d512_half_steps(msd):
     Vo, rc = O.step(rp, cl, Ug, O.gramian(Ug), 0, reg, w, out=V0[rows].copy())
     assert rc == 0
     _check("ials_msd_d512_item", Vg, Vo, rows, ip)
+    _no_slow_path(ctx)
     ctx.close()
 
 
@@ -216,4 +226,5 @@ def test_safer2_2m500k_slice_d1024_half_steps(monkeypatch):
                     entity_reg=full_reg[rows], other_weight=nu_w, out=V0[rows].copy())
     assert rc == 0
     _check("safer2_slice_d1024_item", Vg, Vo, rows, ip)
+    _no_slow_path(ctx)
     ctx.close()
