@@ -38,8 +38,8 @@ $(OBJ)/%.o: $(CSRC)/%.hip $(HDRS)
 $(LIB): $(HIP_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(HIP_OBJS) -lrccl
 
-$(ORACLE): oracle/frecsys_oracle.c oracle/frecsys_oracle.h
-	gcc -O3 -march=native -std=c11 -fPIC -shared -Wall -o $@ oracle/frecsys_oracle.c -lpthread -lm
+$(ORACLE): oracle/frecsys_oracle.c oracle/frecsys_oracle.h oracle/cpu_baseline.c
+	gcc -O3 -march=native -std=c11 -fPIC -shared -Wall -o $@ oracle/frecsys_oracle.c oracle/cpu_baseline.c -lpthread -lm
 
 FRECSYS_HDRS := $(wildcard $(PKG)/include/frecsys/*.h)
 $(RUNMODEL): $(PKG)/tools/run_model.cc $(FRECSYS_HDRS) include/frecsys_hip.h $(LIB)

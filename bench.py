@@ -31,8 +31,10 @@ half-steps, vs 8 TB/s -- the north-star figure at d=512 on the MSD shape.
 loss_gather_roofline: the same bytes of the ComputeUserLoss pass (a pure
 embedding gather) / its time.
 
-cpu_baseline: the CPU restatement (oracle/, kind "port") timing the same U
-half-step on a bounded contiguous user sample on this host's CPU share.
+cpu_baseline: a blocked, vectorised CPU restatement of the reference's Eigen
+path (oracle/cpu_baseline.c, kind "port") timing samples of both half-steps
+on this host's CPU share, projected to one epoch: users per epoch-second,
+like the GPU value.
 
 The shipped library has no knobs that skip work; bench.py refuses to run with
 any FRECSYS_* variable set (they select paths for profiling) unless
@@ -269,36 +271,75 @@ def item_gather_fabric(pmc, ms, n_items, Dp):
             "halfstep_ms": ms}
 
 
-def cpu_baseline(spec, up, uc, V, seconds, nthreads, host):
-    """Oracle U half-step (kind of the workload's U step, Gramian excluded) on
-    a bounded contiguous user sample."""
+def cpu_baseline(spec, up, uc, ip, ic, U, V, seconds, nthreads, host):
+    """The CPU baseline of one Train() epoch, like for like with the GPU
+    `value` (users updated per second of epoch): oracle/cpu_baseline.c (a
+    cache-blocked, AVX-512-vectorised restatement of the reference's Eigen
+    path: blocked SYRK of 128-row batches, blocked LLT) times a contiguous
+    sample of each half-step (U and V, the workload's kinds, Gramians by
+    the oracle); each half-step is projected to the whole side by the
+    SURVEY 8(d) per-entity cost h d (d+1) + d^3 / 3, and the epoch is the
+    sum.  About `seconds` of CPU work in all."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     f = spec["flags"]
-    G = O.gramian(V, nthreads=nthreads)
-    n = len(up) - 1
+    d = spec["dim"]
+    nu, ni = len(up) - 1, len(ip) - 1
+    hu, hi = np.diff(up).astype(np.float64), np.diff(ip).astype(np.float64)
+    t0 = time.perf_counter()
+    G_V = O.gramian(V, nthreads=nthreads)
+    t_gv = time.perf_counter() - t0
     if spec["model"] == "ials":
-        kind, reg, w, extra = 0, f["l2_reg"], f["uobs_weight"], {}
-    else:  # ProjectU with omega = alpha (the first SAFER2 epoch's weights)
-        kind, reg, w = 1, f["l2_reg"], f["uobs_weight"]
-        extra = {"entity_weight": np.full(n, f["alpha"], np.float32)}
-
-    def run(k):
-        ex = {kk: vv[:k] for kk, vv in extra.items()}
+        ukw = dict(kind=0, reg=f["l2_reg"], w=f["uobs_weight"], reg_exp=f["l2_reg_exp"])
+        vkw = dict(ukw)
+        om = None
         t0 = time.perf_counter()
-        O.step(up[:k + 1], uc[:up[k]], V, G, kind, reg, w, nthreads=nthreads, **ex)
-        return time.perf_counter() - t0
+        G_U = O.gramian(U, nthreads=nthreads)
+        t_gu = time.perf_counter() - t0
+    else:  # ProjectU with omega = alpha, ProjectV with nu = omega / |H_u| (the first epoch)
+        om = np.full(nu, f["alpha"], np.float32)
+        hs = np.where(hu > 0, hu, 1.0)
+        nu_w = (om / hs).astype(np.float32)
+        item_reg = np.add.reduceat((1.0 / hs)[ic], ip[:-1]).astype(np.float32)
+        item_reg[hi == 0] = 0.0
+        ukw = dict(kind=1, reg=f["l2_reg"], w=f["uobs_weight"], entity_weight=om)
+        vkw = dict(kind=2, reg=f["l2_reg"], w=f["uobs_weight"], alpha=f["alpha"],
+                   entity_reg=item_reg, other_weight=nu_w)
+        t0 = time.perf_counter()
+        G_U = O.gramian(U, om, nthreads=nthreads)
+        t_gu = time.perf_counter() - t0
 
-    k = min(n, 64)
-    dt = run(k)
-    k2 = int(min(n, max(k, k * seconds / max(dt, 1e-6))))
-    dt = run(k2)
-    return {"value": k2 / dt, "unit": "user-solve updates/s", "cores": nthreads, "kind": "port",
-            "host": host,
-            "sample": f"oracle {spec['model']} U half-step (kind {kind}, Gramian excluded) on "
-                      f"users 0..{k2 - 1} of the same synthetic {spec['shape']}-shaped data, "
-                      f"d={spec['dim']}, {dt:.1f} s on {nthreads} threads; a faithful fp32 C "
-                      f"restatement (naive SYRK + unblocked LLT), not Eigen itself"}
+    def cost(h):
+        return float(np.sum(np.where(h > 0, h * d * (d + 1.0) + d ** 3 / 3.0, 0.0)))
+
+    def half(ptr, col, X, G, kw, n, budget):
+        def run(k):
+            ex = {kk: (vv[:k] if kk in ("entity_weight", "entity_reg") else vv)
+                  for kk, vv in kw.items()}
+            t = time.perf_counter()
+            O.baseline_step(ptr[:k + 1], col[:ptr[k]], X, G, nthreads=nthreads, **ex)
+            return time.perf_counter() - t
+        k = min(n, 64)
+        dt = run(k)
+        k2 = int(min(n, max(k, k * budget / max(dt, 1e-6))))
+        dt = run(k2)
+        h = np.diff(ptr)
+        return k2, dt, dt * cost(h) / max(cost(h[:k2]), 1.0)
+
+    ku, dtu, tu = half(up, uc, V, G_V, ukw, nu, seconds / 2)
+    kv, dtv, tv = half(ip, ic, U, G_U, vkw, ni, seconds / 2)
+    epoch = tu + tv + t_gu + t_gv
+    return {"value": nu / epoch, "unit": "user-solve updates/s", "cores": nthreads,
+            "kind": "port", "host": host,
+            "sec_per_epoch_projected": epoch,
+            "u_halfstep_updates_per_s": ku / dtu,
+            "sample": f"oracle/cpu_baseline.c (blocked, AVX-512-vectorised restatement of the "
+                      f"reference's Eigen path) on {nthreads} threads: U half-step on users "
+                      f"0..{ku - 1} ({dtu:.1f} s) and V half-step on items 0..{kv - 1} "
+                      f"({dtv:.1f} s) of the same synthetic {spec['shape']}-shaped data, "
+                      f"d={d}, each projected to its whole side by sum(h d (d+1) + d^3/3), "
+                      f"plus both Gramians timed whole ({t_gu + t_gv:.1f} s); epoch "
+                      f"{epoch:.2f} s projected; not Eigen itself"}
 
 
 def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, warmup, cpu_s):
@@ -419,8 +460,9 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
     if cpu_s > 0 and world == 1 and rank == 0:
         try:
             nthreads, host = host_cpu_share()
+            U = ctx.get_embeddings(fh.SIDE_USER)
             V = ctx.get_embeddings(fh.SIDE_ITEM)
-            res["cpu_baseline"] = cpu_baseline(spec, up, uc, V, cpu_s, nthreads, host)
+            res["cpu_baseline"] = cpu_baseline(spec, up, uc, ip, ic, U, V, cpu_s, nthreads, host)
         except Exception as e:  # the baseline must never kill the bench line
             log(f"[bench] cpu baseline failed: {e}")
             res["cpu_baseline"] = None

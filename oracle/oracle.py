@@ -69,6 +69,8 @@ def lib():
             "oracle_uniform_int": (ctypes.c_uint32, [P, ctypes.c_uint32]),
             "oracle_mean": (F, [P, I64]),
             "oracle_safer2_xi_snr": (F, [P, I64, F, ctypes.c_int, F, F, ctypes.c_int, F, P]),
+            "cpu_baseline_step": (I64, [I64, P, P, P, I64, ctypes.c_int, P, ctypes.c_int, F, F, F,
+                                        F, ctypes.c_int, P, P, P, P, ctypes.c_int]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)
@@ -119,6 +121,26 @@ def step(row_ptr, col, X, G, kind, reg, w, reg_exp=1.0, alpha=0.0, stepsize=0.0,
     sp = SolveParams(kind, reg, reg_exp, w, alpha, stepsize, quirk, _p(ew), _p(er), _p(ow))
     rc = lib().oracle_step(n, _p(rp), _p(cl), _p(X), X.shape[0], d, _p(G), ctypes.byref(sp),
                            _p(Ev), _p(out), nthreads)
+    return out, int(rc)
+
+
+def baseline_step(row_ptr, col, X, G, kind, reg, w, reg_exp=1.0, alpha=0.0, quirk=1,
+                  entity_weight=None, entity_reg=None, other_weight=None, out=None, nthreads=1):
+    """The timed CPU baseline (cpu_baseline.c): the same half-step as step()
+    for kinds 0 / 1 / 2, cache-blocked and vectorised like Eigen's path."""
+    rp = np.ascontiguousarray(row_ptr, np.int64)
+    cl = np.ascontiguousarray(col, np.int32)
+    X, G = f32(X), f32(G)
+    n = len(rp) - 1
+    d = X.shape[1]
+    if out is None:
+        out = np.zeros((n, d), np.float32)
+    ew = None if entity_weight is None else f32(entity_weight)
+    er = None if entity_reg is None else f32(entity_reg)
+    ow = None if other_weight is None else f32(other_weight)
+    rc = lib().cpu_baseline_step(n, _p(rp), _p(cl), _p(X), X.shape[0], d, _p(G), kind, reg,
+                                 reg_exp, w, alpha, quirk, _p(ew), _p(er), _p(ow), _p(out),
+                                 nthreads)
     return out, int(rc)
 
 

@@ -121,7 +121,7 @@ __device__ __forceinline__ bool xcd_unit(int P, int64_t n_units, int64_t& unit, 
 // every W2FLUSH chunks).
 constexpr int WB2 = 256;
 constexpr int W2R = 16;
-constexpr int W2RING = 4;
+constexpr int W2RING = 8;
 constexpr int W2FLUSH = 128;
 constexpr int W2GRAN = 6 * 512;  // 16-B granules per stage buffer
 
@@ -132,10 +132,11 @@ int wide_pairs2(int Dp) {
   return nb * (nb + 1) / 2;
 }
 
-template <int MODE, bool OFF64 = false>
+template <int MODE, bool OFF64 = false, int AH = 2>
 __global__ void __launch_bounds__(512)
     wide_syrk2_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws,
                       int64_t n_units) {
+  static_assert(AH == 1 || AH == 2, "rows loaded one or two chunks ahead");
   __shared__ __attribute__((aligned(16))) bf16x8 stage[2][W2GRAN];
   __shared__ __attribute__((aligned(16))) int ring_id[W2RING * W2R];
   __shared__ float2 ring_sb[W2RING * W2R];  // (row scale, rhs / B-side weight)
@@ -220,8 +221,10 @@ __global__ void __launch_bounds__(512)
   const int xcol = sc < WB2 ? WB2 * BI + sc : WB2 * BJ + (sc - WB2);
   const bool wside = MODE == 0 && !same && sc >= WB2;  // weighted B operand
   const bool bown = MODE >= 1 && dgp;                  // diagonal pairs form b
-  float xr[16];
-  auto load = [&](int c) __attribute__((always_inline)) {
+  // AH register sets of the staged rows: chunk c's in set c % AH, loaded AH
+  // iterations before it is staged
+  float xr0[16], xr1[AH == 2 ? 16 : 1];
+  auto load = [&](int c, float (&xr)[16]) __attribute__((always_inline)) {
     const int base = (c % W2RING) * W2R + 8 * hh0;
     const int4* ids4 = reinterpret_cast<const int4*>(ring_id + base);  // base % 8 == 0
 #pragma unroll
@@ -246,7 +249,8 @@ __global__ void __launch_bounds__(512)
   float bpart = 0.0f, btot = 0.0f;
   // staging math of one value (row r of the thread's column): scale, rhs
   // part, 3-piece split into the fragment being assembled
-  auto stage_val = [&](int base, int r, bf16x8 (&f)[3], int j) __attribute__((always_inline)) {
+  auto stage_val = [&](const float (&xr)[16], int base, int r, bf16x8 (&f)[3], int j)
+                       __attribute__((always_inline)) {
     // no contraction: x is the rounded fp32 product in every instantiation
     // (fused into split3's x - hi it would depend on the code around it)
 #pragma clang fp contract(off)
@@ -261,14 +265,14 @@ __global__ void __launch_bounds__(512)
     f[2][j] = pl;
   };
   // the whole chunk at once (prologue)
-  auto stage_write = [&](int buf, int c) __attribute__((always_inline)) {
+  auto stage_write = [&](const float (&xr)[16], int buf, int c) __attribute__((always_inline)) {
     const int base = (c % W2RING) * W2R + 8 * hh0;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       if (same && hh > 0) break;
       bf16x8 f[3];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) stage_val(base, 8 * hh + j, f, j);
+      for (int j = 0; j < 8; ++j) stage_val(xr, base, 8 * hh + j, f, j);
 #pragma unroll
       for (int p = 0; p < 3; ++p) stage[buf][g2(p, hh0 + hh, sc)] = f[p];
     }
@@ -314,7 +318,7 @@ __global__ void __launch_bounds__(512)
 
   if (tid < W2R) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < 2 + AH; ++c)
       if (c < nchunks) {
         int id;
         float sa, bw;
@@ -324,26 +328,31 @@ __global__ void __launch_bounds__(512)
   }
   lds_barrier();
   if (nchunks > 0) {
-    load(0);
-    stage_write(0, 0);
+    load(0, xr0);
+    stage_write(xr0, 0, 0);
   }
-  if (nchunks > 1) load(1);
+  if constexpr (AH == 2) {
+    if (nchunks > 1) load(1, xr1);
+    if (nchunks > 2) load(2, xr0);
+  } else {
+    if (nchunks > 1) load(1, xr0);
+  }
   lds_barrier();
 
   // chunk c: the MFMAs of its tiles, with chunk c+1's staging math (rows
-  // loaded one iteration ago) spread over the gaps between them -- a slice
+  // loaded AH iterations ago) spread over the gaps between them -- a slice
   // of NV/8 values after each tile, a granule group stored once complete --
   // instead of a VALU phase of its own after the MFMAs
-  auto run = [&](auto same_c) __attribute__((always_inline)) {
-    constexpr bool SAME = decltype(same_c)::value;
-    constexpr int NV = SAME ? 8 : 16, PER = NV / MT;
-    for (int c = 0; c < nchunks; ++c) {
+  // iteration c: xr holds chunk c+1 (staged now), and then takes chunk c+AH+1
+  auto body = [&](auto same_c, int c, float (&xr)[16]) __attribute__((always_inline)) {
+      constexpr bool SAME = decltype(same_c)::value;
+      constexpr int NV = SAME ? 8 : 16, PER = NV / MT;
       const int buf = c & 1;
       const bool more = c + 1 < nchunks;
-      const bool ring_more = (tid < W2R) && (c + 3 < nchunks);
+      const bool ring_more = (tid < W2R) && (c + 2 + AH < nchunks);
       int nid = -1;
       float nsa = 0.f, nbw = 0.f;
-      if (ring_more) ring_load(c + 3, nid, nsa, nbw);
+      if (ring_more) ring_load(c + 2 + AH, nid, nsa, nbw);
       const bf16x8* st = stage[buf];
       bf16x8* sto = stage[buf ^ 1];
       const int nbase = ((c + 1) % W2RING) * W2R + 8 * hh0;
@@ -376,7 +385,7 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
           for (int u = 0; u < PER; ++u) {
             const int r = m * PER + u;
-            stage_val(nbase, r, fs, r & 7);
+            stage_val(xr, nbase, r, fs, r & 7);
           }
           if ((m * PER + PER) % 8 == 0) {
             const int hh = (m * PER) >> 3;
@@ -392,12 +401,21 @@ __global__ void __launch_bounds__(512)
       // load between -- was vmcnt(0), wave 0 stalling on the rows it had just
       // requested (a full HBM latency per chunk, every wave behind it at the
       // barrier)
-      if (ring_more) ring_store(c + 3, nid, nsa, nbw);
+      if (ring_more) ring_store(c + 2 + AH, nid, nsa, nbw);
       // unconditional (past the end it re-gathers the last chunk, whose ring
       // slot stays valid; never staged): a conditional load here made the
       // waitcnt pass flush vmcnt at the loop head, stalling on these rows
-      load(c + 2 < nchunks ? c + 2 : nchunks - 1);
+      load(c + 1 + AH < nchunks ? c + 1 + AH : nchunks - 1, xr);
       lds_barrier();
+  };
+  auto run = [&](auto same_c) __attribute__((always_inline)) {
+    if constexpr (AH == 2) {
+      for (int c = 0; c < nchunks; c += 2) {
+        body(same_c, c, xr1);
+        if (c + 1 < nchunks) body(same_c, c + 1, xr0);
+      }
+    } else {
+      for (int c = 0; c < nchunks; ++c) body(same_c, c, xr0);
     }
   };
   if (same) run(std::true_type{});
@@ -1347,6 +1365,16 @@ __global__ void __launch_bounds__(256) loss_gather_wide_kernel(LossArgs a) {
   if (lane == 0) a.out[e] = loss;
 }
 
+// FRECSYS_W2_AHEAD=2: the d-space SYRK loads rows two chunks ahead instead
+// of one (A/B of the prefetch depth)
+bool w2_ahead1() {
+  static const bool v = [] {
+    const char* e = getenv("FRECSYS_W2_AHEAD");
+    return !(e && atoi(e) == 2);
+  }();
+  return v;
+}
+
 unsigned xcd_grid(int64_t n_units, int P) { return (unsigned)(((n_units + 7) / 8) * 8 * P); }
 
 size_t wide_chol_lds_bytes(int Dp) {
@@ -1423,6 +1451,9 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
     if (off64)
       hipLaunchKernelGGL((wide_syrk2_kernel<2, true>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
+    else if (w2_ahead1())
+      hipLaunchKernelGGL((wide_syrk2_kernel<2, false, 1>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
     else
       hipLaunchKernelGGL((wide_syrk2_kernel<2, false>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
@@ -1431,6 +1462,9 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
     const int64_t nb = std::min<int64_t>(batch, a.n_rows - s0);
     if (off64)
       hipLaunchKernelGGL((wide_syrk2_kernel<1, true>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
+    else if (w2_ahead1())
+      hipLaunchKernelGGL((wide_syrk2_kernel<1, false, 1>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     else
       hipLaunchKernelGGL((wide_syrk2_kernel<1, false>), dim3(xcd_grid(nb, wide_pairs2(Dp))),

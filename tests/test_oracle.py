@@ -22,7 +22,7 @@ import pytest
 
 import numpy_ref as R
 import oracle as O
-from conftest import make_quirk_data
+from conftest import make_quirk_data, rel_rows
 
 K_LIST = (5, 10, 20, 50, 100)
 
@@ -280,3 +280,33 @@ def test_eigen_mean_restatement(n):
         for v in x[al:]:
             r = f(r + v)
     assert np.float32(m) == np.float32(r / f(n))
+
+
+@pytest.mark.parametrize("dim", [8, 50, 256])
+def test_cpu_baseline_matches_oracle(quirk_data, dim):
+    """The timed CPU baseline (oracle/cpu_baseline.c: blocked SYRK, blocked
+    LLT with an explicit panel inverse) computes the same half-steps as the
+    oracle (kinds 0 / 1 / 2, tail quirk on) within rounding."""
+    nu, ni, up, uc, ip, ic = quirk_data
+    U, V = O.init_embeddings(1, 0.1, dim, nu, ni)
+    G = O.gramian(V)
+    hu = np.diff(up)
+    Uo, rc = O.step(up, uc, V, G, 0, 0.003, 0.1, out=U.copy())
+    Ub, rc2 = O.baseline_step(up, uc, V, G, 0, 0.003, 0.1, out=U.copy(), nthreads=4)
+    assert rc == rc2 == 0
+    assert rel_rows(Ub[hu > 0], Uo[hu > 0]).max() < 1e-4
+    om = (0.05 + 0.95 * np.random.default_rng(5).random(nu)).astype(np.float32)
+    Uo, _ = O.step(up, uc, V, G, 1, 0.004, 0.004, entity_weight=om, out=U.copy())
+    Ub, _ = O.baseline_step(up, uc, V, G, 1, 0.004, 0.004, entity_weight=om, out=U.copy(),
+                            nthreads=4)
+    assert rel_rows(Ub[hu > 0], Uo[hu > 0]).max() < 1e-4
+    hs = np.where(hu > 0, hu, 1).astype(np.float32)
+    nuw = (om / hs).astype(np.float32)
+    er = np.add.reduceat((1.0 / hs.astype(np.float64))[ic], ip[:-1]).astype(np.float32)
+    Gw = O.gramian(U, om)
+    hi = np.diff(ip)
+    Vo, _ = O.step(ip, ic, U, Gw, 2, 0.004, 0.004, alpha=0.3, entity_reg=er, other_weight=nuw,
+                   out=V.copy())
+    Vb, _ = O.baseline_step(ip, ic, U, Gw, 2, 0.004, 0.004, alpha=0.3, entity_reg=er,
+                            other_weight=nuw, out=V.copy(), nthreads=4)
+    assert rel_rows(Vb[hi > 0], Vo[hi > 0]).max() < 1e-4
