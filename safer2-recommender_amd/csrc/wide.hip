@@ -648,7 +648,14 @@ __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, fl
 // against ~T^3/3 reads and T^3/3 writes of a right-looking update sweep
 // (round 2's kernel: MSD 174 GB of workspace traffic per epoch, 37 ms; this
 // one 30.5 ms).  Compiled for two workgroups per CU (128 registers).
-template <int T>
+// RD = true: the DIAGONAL tiles are updated right-looking instead -- the
+// worker that forms L_Ip (I > p) also applies D_I -= L_Ip L_Ip^T to tile
+// (I, I) in the workspace, reading L_Ip back in the operand layout row p
+// of L has in LDS -- so wave 0's chain loads a finished D_p and only
+// factors it (the p serial tile products of its update leave the chain).
+// The same MFMAs on the same operands in the same order, the running sum
+// passing through fp32 memory between panels: bit-identical to RD = false.
+template <int T, bool RD = false>
 __global__ void __launch_bounds__(512)
     __attribute__((amdgpu_waves_per_eu(T == 16 ? FRECSYS_WIDE_CHOL_WPE : 2, 8)))
     wide_chol_kernel(SolveArgs a, int64_t pos0, float* ws) {
@@ -754,11 +761,13 @@ __global__ void __launch_bounds__(512)
       f32x16 d;
 #pragma unroll
       for (int q = 0; q < 16; ++q) d[q] = App[acc_row(q, hi) * 32 + lo];
+      if constexpr (!RD) {
 #pragma unroll 1
-      for (int q = 0; q < p; ++q) {  // d -= L_pq L_pq^T (k = 16 hi + s)
-        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+        for (int q = 0; q < p; ++q) {  // d -= L_pq L_pq^T (k = 16 hi + s)
+          const float* P = rowL + q * LP + lo * 33 + 16 * hi;
 #pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
+          for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
+        }
       }
       // opaque copies of the lane coordinates: the 48 swizzled / padded
       // addresses below are formed here with a few VALU ops each, not hoisted
@@ -814,6 +823,26 @@ __global__ void __launch_bounds__(512)
         float* Lw = gtile(I, p);
 #pragma unroll
         for (int q = 0; q < 16; ++q) Lw[acc_row(q, hi) * 32 + lo] = l[q];
+        if constexpr (RD) {
+          // D_I -= L_Ip L_Ip^T: L_Ip read back (this wave's own stores) as
+          // row lo, k = 16 hi + s -- rowL's layout for wave 0's update
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          const f32x4v* Lr = reinterpret_cast<const f32x4v*>(Lw + lo * 32 + 16 * hi);
+          f32x4v lr[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) lr[j] = Lr[j];
+          float* Dw = gtile(I, I);
+          f32x16 dI;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) dI[q] = Dw[acc_row(q, hi) * 32 + lo];
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2) {
+            const float v = lr[s2 >> 2][s2 & 3];
+            dI = mfma32(-v, v, dI);
+          }
+#pragma unroll
+          for (int q = 0; q < 16; ++q) Dw[acc_row(q, hi) * 32 + lo] = dI[q];
+        }
       }
     }
     __syncthreads();
@@ -1366,13 +1395,17 @@ __global__ void __launch_bounds__(256) loss_gather_wide_kernel(LossArgs a) {
 }
 
 // FRECSYS_W2_AHEAD=2: the d-space SYRK loads rows two chunks ahead instead
-// of one (A/B of the prefetch depth)
+// of one (A/B of the prefetch depth; read at each call)
 bool w2_ahead1() {
-  static const bool v = [] {
-    const char* e = getenv("FRECSYS_W2_AHEAD");
-    return !(e && atoi(e) == 2);
-  }();
-  return v;
+  const char* e = getenv("FRECSYS_W2_AHEAD");
+  return !(e && atoi(e) == 2);
+}
+
+// FRECSYS_WIDE_CHOL_RD=1: right-looking diagonal updates in the wide
+// Cholesky (A/B; bit-identical; read at each call)
+bool wide_chol_rd() {
+  const char* e = getenv("FRECSYS_WIDE_CHOL_RD");
+  return e && atoi(e) != 0;
 }
 
 unsigned xcd_grid(int64_t n_units, int P) { return (unsigned)(((n_units + 7) / 8) * 8 * P); }
@@ -1437,6 +1470,10 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(512));
     if (err == hipSuccess)
+      err = hipFuncSetAttribute((const void*)wide_chol_kernel<16, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)wide_chol_lds_bytes(512));
+    if (err == hipSuccess)
       err = hipFuncSetAttribute((const void*)wide_chol_kernel<32>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(1024));
@@ -1471,6 +1508,9 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
+    else if (Dp == 512 && wide_chol_rd())
+      hipLaunchKernelGGL((wide_chol_kernel<16, true>), dim3((unsigned)nb), dim3(512),
+                         wide_chol_lds_bytes(Dp), s, a, s0, ws);
     else if (Dp == 512)
       hipLaunchKernelGGL(wide_chol_kernel<16>, dim3((unsigned)nb), dim3(512),
                          wide_chol_lds_bytes(Dp), s, a, s0, ws);
