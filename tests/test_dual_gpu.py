@@ -7,6 +7,7 @@ entity, FRECSYS_DUAL_MAX_H moves the split between the two paths.
 import numpy as np
 import pytest
 
+import numpy_ref as R
 import oracle as O
 from conftest import rel_rows
 from test_models_gpu import report
@@ -117,19 +118,35 @@ def test_chol_basis_conditioning(monkeypatch, quirk_data, dim, reg, w):
         assert ctx.work("basis_chol")[2] == (on == "1")
         outs.append(ctx.get_embeddings(fh.SIDE_USER))
         ctx.close()
-    Uo, rc = O.step(up, uc, V0, O.gramian(V0), 0, reg, w, reg_exp=0.0, out=U.copy())
+    G0 = O.gramian(V0)
+    Uo, rc = O.step(up, uc, V0, G0, 0, reg, w, reg_exp=0.0, out=U.copy())
     assert rc == 0
     h = np.diff(up)
     hs = (h > 0) & (h <= 256)
     e_chol = rel_rows(outs[0][hs], Uo[hs]).max()
     e_tri = rel_rows(outs[1][hs], Uo[hs]).max()
-    print(f"dim {dim} reg {reg} w {w}: chol {e_chol:.2e} tridiag {e_tri:.2e}")
+    # every path against the float64 solution of the same (fp32-rounded)
+    # inputs: on the quirk fixture's 400 items G is singular at d = 512
+    # (rank <= 400), so with lambda = reg alone cond(A) reaches ~1e4 - 1e8 and
+    # two fp32 computations differ by cond x eps whatever their order; the bar
+    # there is accuracy -- each GPU basis no worse than the oracle's own fp32
+    # restatement of the reference -- and the 1e-4 oracle bar where the
+    # conditioning allows it
+    rows = np.nonzero(hs)[0]
+    X64 = np.array([R.ials(uc[up[r]:up[r + 1]], V0, G0, reg, w) for r in rows])
+    f_or = rel_rows(Uo[rows], X64).max()
+    f_chol = rel_rows(outs[0][rows], X64).max()
+    f_tri = rel_rows(outs[1][rows], X64).max()
+    print(f"dim {dim} reg {reg} w {w}: vs oracle chol {e_chol:.2e} tridiag {e_tri:.2e}; "
+          f"vs float64 oracle {f_or:.2e} chol {f_chol:.2e} tridiag {f_tri:.2e}")
     report(test="chol_basis_conditioning", dim=dim, reg=reg, w=w, chol=float(e_chol),
-           tridiag=float(e_tri))
-    assert e_chol < max(TOL_ROW, 3.0 * e_tri), (e_chol, e_tri)
-    # the tridiagonal basis is the one every benchmarked config uses: it is
-    # held to the row bar itself, ill-conditioned M included
-    assert e_tri < TOL_ROW, e_tri
+           tridiag=float(e_tri), f64_oracle=float(f_or), f64_chol=float(f_chol),
+           f64_tridiag=float(f_tri))
+    assert f_chol <= max(TOL_ROW, 2.0 * f_or), (f_chol, f_or)
+    # the tridiagonal basis is the one every benchmarked config uses
+    assert f_tri <= max(TOL_ROW, 2.0 * f_or), (f_tri, f_or)
+    if f_or < 1e-5:  # well conditioned: the row bar against the oracle itself
+        assert e_chol < TOL_ROW and e_tri < TOL_ROW, (e_chol, e_tri)
 
 
 @pytest.mark.parametrize("dim", [64, 128, 256])
