@@ -219,10 +219,20 @@ int frecsys_pp_predict(frecsys_ctx* ctx, int32_t side);
  * (safer2pp.h:449-653, 97-216; entity_weight / entity_reg + other_weight +
  * alpha as for frecsys_solve_side, G[other] the omega-weighted Gramian for
  * WEIGHTED_V).  Updates the block of the rows and their predictions.
- * Every rank runs every row (replicas: the prediction vector is not
- * sharded).  residual (may be NULL): sum of squared block deltas. */
+ * At world > 1 (USER / ITEM) each rank solves its own shard of the rows
+ * (frecsys_shard_range); with RCCL the rows are then all-gathered and every
+ * rank replays the other ranks' prediction updates from them, so the
+ * prediction vector and the embeddings are bitwise the single-rank ones;
+ * without a communicator (external exchange) the caller copies the other
+ * ranks' rows in (frecsys_set_embeddings) and calls frecsys_pp_sync.
+ * residual (may be NULL): sum of squared block deltas (over every rank's
+ * rows with RCCL, this rank's rows otherwise). */
 int frecsys_pp_step(frecsys_ctx* ctx, int32_t side, int32_t start, int32_t end,
                     const frecsys_solve_params* params, double* residual);
+/* External-exchange completion of a sharded frecsys_pp_step on `side`: after
+ * the other ranks' rows were set, apply their block updates to this rank's
+ * prediction vector.  No reference counterpart (the sharded path is new). */
+int frecsys_pp_sync(frecsys_ctx* ctx, int32_t side);
 /* Fold-in evaluation ranking (replaces the scoring + top-K of
  * EvaluateDatasetInternal / EvaluateUser, recommender.h:78-199): for every
  * row r of the EVAL side, scores s = V u_r over all items (fp32), the items

@@ -124,6 +124,12 @@ struct frecsys_ctx {
   size_t cap_pred[2] = {0, 0};
   float* d_resid = nullptr;
   size_t cap_resid = 0;
+  // sharded iALS++ / SAFER2++ block steps: the block columns of the side's
+  // rows before the step ([n][bw]), for the prediction refresh of the rows
+  // other ranks solve (frecsys_pp_step with RCCL; frecsys_pp_sync without)
+  float* d_pp_old = nullptr;
+  size_t cap_pp_old = 0;
+  int pp_old_side = -1, pp_old_start = 0, pp_old_bw = 0;
   float* d_rows = nullptr;       // train stats: per-row values
   size_t cap_rows = 0;
   float* d_gstat = nullptr;      // train stats: U^T U, V^T V
@@ -1943,8 +1949,26 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
                 (size_t)c->n[other]);
     if (rc) return rc;
   }
-  // every rank runs every row: the work queue of the whole side
-  const int64_t lo = 0, hi = c->n[side];
+  // world > 1 (USER / ITEM): this rank's shard of the rows -- the per-row
+  // block steps are independent given the predictions, which every rank then
+  // brings up to date for the other ranks' rows (pp_refresh_kernel, bitwise
+  // the owner's update); EVAL rows are not sharded
+  const bool sharded = side < 2 && c->world > 1;
+  int64_t lo = 0, hi = c->n[side];
+  if (sharded) shard(c, side, &lo, &hi);
+  const int bw = end - start;
+  if (sharded) {
+    int rc = ensure(c, &c->d_pp_old, &c->cap_pp_old,
+                    (size_t)std::max<int64_t>(c->n[side], 1) * bw);
+    if (rc) return rc;
+    if (c->n[side])
+      HIP_TRY(c, hipMemcpy2DAsync(c->d_pp_old, sizeof(float) * bw, c->emb[side] + start,
+                                  sizeof(float) * c->Dp, sizeof(float) * bw, c->n[side],
+                                  hipMemcpyDeviceToDevice, c->stream));
+    c->pp_old_side = side;
+    c->pp_old_start = start;
+    c->pp_old_bw = bw;
+  }
   std::vector<QueueRec> recs((size_t)(hi - lo));
   const std::vector<int64_t>& rp = side == 2 ? c->host_rp_eval : c->host_rp[side];
   for (int64_t i = lo; i < hi; ++i) recs[i - lo] = QueueRec{(int32_t)i, (int32_t)(rp[i + 1] - rp[i]), rp[i]};
@@ -1979,8 +2003,17 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
   {
     ScopedTimer t(c, "pp_step");
     HIP_TRY(c, launch_pp_step(a, c->stream));
+    if (sharded && c->comm) {
+      // the rows of every rank, then the other ranks' prediction updates
+      rc = allgather_rows(c, c->emb[side], side, c->Dp);
+      if (rc) return rc;
+      HIP_TRY(c, launch_pp_refresh(a, c->rp[side], c->d_pp_old, c->n[side], lo, hi, c->stream));
+      c->pp_old_side = -1;
+    }
     t.stop();
   }
+  if (sharded && c->comm)  // every rank takes the same NOT_SPD verdict
+    NCCL_TRY(c, ncclAllReduce(c->d_fail, c->d_fail, 1, ncclUint64, ncclMin, c->comm, c->stream));
   std::vector<float> res(recs.size());
   unsigned long long f = none;
   HIP_TRY(c, hipMemcpyAsync(&f, c->d_fail, sizeof(f), hipMemcpyDeviceToHost, c->stream));
@@ -1996,8 +2029,32 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
   if (residual) {
     double s = 0.0;
     for (float v : res) s += (double)v;  // zero rows (empty histories) stay 0
+    if (sharded && c->comm) {  // the sum over every rank's rows
+      rc = ensure(c, &c->d_dot, &c->cap_dot, 1);
+      if (rc) return rc;
+      HIP_TRY(c, hipMemcpyAsync(c->d_dot, &s, sizeof(double), hipMemcpyHostToDevice, c->stream));
+      NCCL_TRY(c, ncclAllReduce(c->d_dot, c->d_dot, 1, ncclFloat64, ncclSum, c->comm, c->stream));
+      HIP_TRY(c, hipMemcpyAsync(&s, c->d_dot, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
     *residual = s;
   }
+  return FRECSYS_OK;
+}
+
+int frecsys_pp_sync(frecsys_ctx* c, int32_t side) {
+  if (!c || (side != 0 && side != 1)) return fail(c, FRECSYS_ERR_INVALID, "pp_sync: bad side");
+  if (c->pp_old_side != side)
+    return fail(c, FRECSYS_ERR_INVALID, "pp_sync: no sharded block step of this side pending");
+  HIP_TRY(c, hipSetDevice(c->device));
+  int64_t lo, hi;
+  shard(c, side, &lo, &hi);
+  PPArgs a = pp_args(c, side);
+  a.start = c->pp_old_start;
+  a.bw = c->pp_old_bw;
+  HIP_TRY(c, launch_pp_refresh(a, c->rp[side], c->d_pp_old, c->n[side], lo, hi, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->pp_old_side = -1;
   return FRECSYS_OK;
 }
 

@@ -250,6 +250,10 @@ struct PPArgs {
   float* resid;             // [n_rows] squared delta norms, or nullptr
   unsigned long long* fail;
 };
+// Sharded block step: the prediction updates of rows [0, n) outside [lo, hi)
+// replayed from old ([n][bw], the block before the step) and a.E (after).
+hipError_t launch_pp_refresh(const PPArgs& a, const int64_t* row_ptr, const float* old,
+                             int64_t n, int64_t lo, int64_t hi, hipStream_t s);
 hipError_t launch_pp_step(const PPArgs& a, hipStream_t s);
 // PredictDataset over the CSR rows 0..n_rows-1 (E = the rows' embeddings).
 hipError_t launch_pp_predict(const PPArgs& a, const int64_t* row_ptr, int64_t n_rows,

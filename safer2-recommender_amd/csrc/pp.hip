@@ -182,7 +182,8 @@ __global__ void __launch_bounds__(256) pp_block_kernel(PPArgs a) {
   for (int64_t k = wave; k < h; k += 4) {  // ialspp.h:400-404
     const int id = a.col[p0 + k];
     float t = 0.0f;
-    for (int c = lane; c < bw; c += 64) t += xvec[c] * a.X[(int64_t)id * Dp + s0 + c];
+    // explicit fma: pp_refresh_kernel repeats this sum bit for bit
+    for (int c = lane; c < bw; c += 64) t = __builtin_fmaf(xvec[c], a.X[(int64_t)id * Dp + s0 + c], t);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
     if (lane == 0) a.pred[a.rix ? a.rix[p0 + k] : p0 + k] += t;
@@ -208,7 +209,48 @@ __global__ void __launch_bounds__(256) pp_predict_kernel(PPArgs a, const int64_t
   }
 }
 
+// Sharded block step (world > 1): the prediction updates of the rows other
+// ranks solved, replayed from the all-gathered rows -- dl = new - old of the
+// block (old: [n][bw] snapshot taken before the step), then per rating the
+// same per-lane fma chain and butterfly sum as pp_block_kernel, so every
+// rank's prediction vector is bitwise the single-rank one.  One wave per row
+// of [0, n) outside [lo, hi).
+__global__ void __launch_bounds__(256) pp_refresh_kernel(PPArgs a, const int64_t* row_ptr,
+                                                         const float* old, int64_t n, int64_t lo,
+                                                         int64_t hi) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= n || (r >= lo && r < hi)) return;
+  const int Dp = a.Dp, s0 = a.start, bw = a.bw;
+  float dl[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = lane + 64 * j;
+    dl[j] = c < bw ? a.E[r * Dp + s0 + c] - old[r * bw + c] : 0.0f;
+  }
+  for (int64_t k = row_ptr[r]; k < row_ptr[r + 1]; ++k) {
+    const float* x = a.X + (int64_t)a.col[k] * Dp + s0;
+    float t = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = lane + 64 * j;
+      if (c < bw) t = __builtin_fmaf(dl[j], x[c], t);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (lane == 0) a.pred[a.rix ? a.rix[k] : k] += t;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_pp_refresh(const PPArgs& a, const int64_t* row_ptr, const float* old,
+                             int64_t n, int64_t lo, int64_t hi, hipStream_t s) {
+  if (n <= 0 || (lo == 0 && hi >= n)) return hipSuccess;
+  hipLaunchKernelGGL(pp_refresh_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, a,
+                     row_ptr, old, n, lo, hi);
+  return hipGetLastError();
+}
 
 hipError_t launch_pp_step(const PPArgs& a, hipStream_t s) {
   if (a.n_rows <= 0) return hipSuccess;

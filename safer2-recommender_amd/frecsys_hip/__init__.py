@@ -40,6 +40,7 @@ EXPORTS = (
     "frecsys_history_space_max_h", "frecsys_comm_world", "frecsys_gram_groups",
     "frecsys_get_gram_groups", "frecsys_set_gram_groups", "frecsys_get_gramian",
     "frecsys_gram_plan", "frecsys_work", "frecsys_snapshot_residual", "frecsys_counter",
+    "frecsys_pp_sync",
 )
 
 # Every symbol include/frecsys_model.h declares.
@@ -140,6 +141,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_pp_step": (ctypes.c_int, [P, I32, I32, I32, P, P]),
         "frecsys_snapshot_residual": (ctypes.c_int, [P, I32, P]),
         "frecsys_counter": (ctypes.c_int, [P, ctypes.c_char_p, P]),
+        "frecsys_pp_sync": (ctypes.c_int, [P, I32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -418,6 +420,10 @@ class Context:
     def pp_set_rating_index(self, side: int, rix: np.ndarray):
         r = np.ascontiguousarray(rix, dtype=np.int32)
         self._check(self.lib.frecsys_pp_set_rating_index(self.h, side, _ptr(r)))
+
+    def pp_sync(self, side: int):
+        """External-exchange completion of a sharded pp_step (frecsys_pp_sync)."""
+        self._check(self.lib.frecsys_pp_sync(self.h, side))
 
     def pp_predict(self, side: int):
         self._check(self.lib.frecsys_pp_predict(self.h, side))

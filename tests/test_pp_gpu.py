@@ -158,3 +158,80 @@ def test_gate_safer2pp_run_model():  # safer2pp_test.cc:100-145
     assert m and float(m.group(1)) >= 0.2, tail[-2000:]
     means = [float(x) for x in re.findall(r"Min: [0-9.]+, Mean: ([0-9.]+), Max", r.stderr)]
     assert len(means) == 10 and all(abs(x - 0.3) <= 0.02 for x in means), means
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("dim,bs,kind", [(64, 24, fh.KIND_IALS), (256, 128, fh.KIND_IALS),
+                                          (64, 32, fh.KIND_WEIGHTED_U)])
+def test_pp_sharded_bitwise(quirk_data, world, dim, bs, kind):
+    """Sharded iALS++ / SAFER2++ block steps: W contexts on cuda:0 joined as
+    ranks in external-exchange mode each solve their own rows; the test does
+    what RCCL does (Gramian group slabs, the rows), and every rank replays
+    the others' prediction updates (frecsys_pp_sync).  Embeddings after a
+    full epoch of user + item block steps equal the single-rank run BIT FOR
+    BIT, and the residual sums over the ranks."""
+    from test_parity_gpu import _v_inputs, _weights
+    from test_sharded_gpu import _allgather_rows, _allreduce_gram
+    nu, ni, up, uc, ip, ic = quirk_data
+    reg, w, alpha = 0.003, 0.1, 0.3
+    urix, irix = _rix(uc)
+    om = _weights(nu)
+    nu_w, item_reg = _v_inputs(nu, ni, up, ip, ic, om)
+
+    def make(W, r):
+        c = fh.Context(dim, nu, ni, device=0)
+        if W > 1:
+            c.comm_init(W, r, None)
+        c.load_csr(fh.SIDE_USER, up, uc)
+        c.load_csr(fh.SIDE_ITEM, ip, ic)
+        c.init_embeddings(1, 0.1)
+        c.pp_set_rating_index(fh.SIDE_USER, urix)
+        c.pp_set_rating_index(fh.SIDE_ITEM, irix)
+        c.pp_predict(fh.SIDE_USER)
+        return c
+
+    def ukw():
+        return dict(kind=kind, entity_weight=om) if kind == fh.KIND_WEIGHTED_U else {}
+
+    def vkw():
+        if kind == fh.KIND_WEIGHTED_U:
+            return dict(kind=fh.KIND_WEIGHTED_V, alpha=alpha, entity_reg=item_reg,
+                        other_weight=nu_w)
+        return {}
+
+    gw = om if kind == fh.KIND_WEIGHTED_U else None
+    ref = make(1, 0)
+    ctxs = [make(world, r) for r in range(world)]
+    for start in range(0, dim, bs):
+        end = min(start + bs, dim)
+        ref.gramian(fh.SIDE_ITEM)
+        r_ref = ref.pp_step(fh.SIDE_USER, start, end, reg, w, **ukw())
+        _allreduce_gram(ctxs, fh.SIDE_ITEM)
+        r_sh = sum(c.pp_step(fh.SIDE_USER, start, end, reg, w, **ukw()) for c in ctxs)
+        _allgather_rows(ctxs, fh.SIDE_USER)
+        for c in ctxs:
+            c.pp_sync(fh.SIDE_USER)
+        assert abs(r_sh - r_ref) <= 1e-9 * max(r_ref, 1e-30)
+        ref.gramian(fh.SIDE_USER, weights=gw)
+        ref.pp_step(fh.SIDE_ITEM, start, end, reg, w, **vkw())
+        _allreduce_gram(ctxs, fh.SIDE_USER, gw)
+        for c in ctxs:
+            c.pp_step(fh.SIDE_ITEM, start, end, reg, w, **vkw())
+        _allgather_rows(ctxs, fh.SIDE_ITEM)
+        for c in ctxs:
+            c.pp_sync(fh.SIDE_ITEM)
+    Ur, Vr = ref.get_embeddings(fh.SIDE_USER), ref.get_embeddings(fh.SIDE_ITEM)
+    for c in ctxs:
+        np.testing.assert_array_equal(c.get_embeddings(fh.SIDE_USER), Ur)
+        np.testing.assert_array_equal(c.get_embeddings(fh.SIDE_ITEM), Vr)
+    # the predictions too: the next block step of every rank reads them
+    ref.gramian(fh.SIDE_ITEM)
+    r_ref = ref.pp_step(fh.SIDE_USER, 0, min(bs, dim), reg, w, **ukw())
+    _allreduce_gram(ctxs, fh.SIDE_ITEM)
+    for c in ctxs:
+        c.pp_step(fh.SIDE_USER, 0, min(bs, dim), reg, w, **ukw())
+    _allgather_rows(ctxs, fh.SIDE_USER)
+    np.testing.assert_array_equal(ctxs[0].get_embeddings(fh.SIDE_USER),
+                                  ref.get_embeddings(fh.SIDE_USER))
+    for c in ctxs + [ref]:
+        c.close()
