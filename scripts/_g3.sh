@@ -2,7 +2,7 @@ set -o pipefail
 OUT=gpurun_out/r4a
 mkdir -p $OUT
 fatal() { case $1 in 124|137|134|139|143) return 0;; esac; return 1; }
-timeout -k 10 600 python -u -m pytest -v -s --timeout 300 --timeout-method thread tests/test_wide_split_gpu.py tests/test_dual_gpu.py -k "variants or conditioning" > $OUT/pytest_ah2.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest -v -s --timeout 300 --timeout-method thread tests/test_wide_split_gpu.py tests/test_dual_gpu.py tests/test_pp_gpu.py -k "variants or conditioning or sharded" > $OUT/pytest_ah2.log 2>&1; rc=$?
 tail -3 $OUT/pytest_ah2.log
 fatal $rc && exit $rc
 bash scripts/msd_prof.sh r4a/msd
