@@ -655,9 +655,11 @@ __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, fl
 // factors it (the p serial tile products of its update leave the chain).
 // The same MFMAs on the same operands in the same order, the running sum
 // passing through fp32 memory between panels: bit-identical to RD = false.
-template <int T, bool RD = false>
+// FB = true: the MFMA-blocked diagonal factor (chol.h diag_factor_inv_blk),
+// which needs the register budget of one workgroup per CU (WPE = 2).
+template <int T, bool RD = false, int WPE = (T == 16 ? FRECSYS_WIDE_CHOL_WPE : 2), bool FB = false>
 __global__ void __launch_bounds__(512)
-    __attribute__((amdgpu_waves_per_eu(T == 16 ? FRECSYS_WIDE_CHOL_WPE : 2, 8)))
+    __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     wide_chol_kernel(SolveArgs a, int64_t pos0, float* ws) {
   constexpr int Dp = 32 * T, NT = T * (T + 1) / 2, NW = 8;
   typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -779,7 +781,7 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
       for (int q = 0; q < 16; ++q) dinv[sw(acc_row(q, hi_o), lo_o)] = d[q];
       wave_lds_sync();
-      if (!diag_factor_inv(dinv, lane) && lane == 0) flag[0] = 1;
+      if (!diag_factor_inv<FB>(dinv, lane) && lane == 0) flag[0] = 1;
       wave_lds_sync();
       float* Aw = gtile(p, p);  // L_pp^-1 for the back substitution, and its padded copy
 #pragma unroll
@@ -1402,10 +1404,11 @@ bool w2_ahead1() {
 }
 
 // FRECSYS_WIDE_CHOL_RD=1: right-looking diagonal updates in the wide
-// Cholesky (A/B; bit-identical; read at each call)
-bool wide_chol_rd() {
+// Cholesky (A/B; bit-identical; read at each call); =2: the same with the
+// MFMA-blocked diagonal factor at one workgroup per CU
+int wide_chol_rd() {
   const char* e = getenv("FRECSYS_WIDE_CHOL_RD");
-  return e && atoi(e) != 0;
+  return e ? atoi(e) : 0;
 }
 
 unsigned xcd_grid(int64_t n_units, int P) { return (unsigned)(((n_units + 7) / 8) * 8 * P); }
@@ -1474,6 +1477,10 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(512));
     if (err == hipSuccess)
+      err = hipFuncSetAttribute((const void*)wide_chol_kernel<16, true, 2, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)wide_chol_lds_bytes(512));
+    if (err == hipSuccess)
       err = hipFuncSetAttribute((const void*)wide_chol_kernel<32>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(1024));
@@ -1508,6 +1515,9 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
+    else if (Dp == 512 && wide_chol_rd() == 2)
+      hipLaunchKernelGGL((wide_chol_kernel<16, true, 2, true>), dim3((unsigned)nb), dim3(512),
+                         wide_chol_lds_bytes(Dp), s, a, s0, ws);
     else if (Dp == 512 && wide_chol_rd())
       hipLaunchKernelGGL((wide_chol_kernel<16, true>), dim3((unsigned)nb), dim3(512),
                          wide_chol_lds_bytes(Dp), s, a, s0, ws);
