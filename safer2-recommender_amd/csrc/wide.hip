@@ -657,7 +657,12 @@ __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, fl
 // passing through fp32 memory between panels: bit-identical to RD = false.
 // FB = true: the MFMA-blocked diagonal factor (chol.h diag_factor_inv_blk),
 // which needs the register budget of one workgroup per CU (WPE = 2).
-template <int T, bool RD = false, int WPE = (T == 16 ? FRECSYS_WIDE_CHOL_WPE : 2), bool FB = false>
+// ST = true (with RD): no staging of row p of L in LDS -- every L_pq operand
+// is streamed from the workspace like L_Iq (L1 / L2 hits: the seven workers
+// read the same row), so a panel has no load phase and no barrier before its
+// products; the same values in the same order (bit-identical to ST = false).
+template <int T, bool RD = false, int WPE = (T == 16 ? FRECSYS_WIDE_CHOL_WPE : 2), bool FB = false,
+          bool ST = false>
 __global__ void __launch_bounds__(512)
     __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     wide_chol_kernel(SolveArgs a, int64_t pos0, float* ws) {
@@ -700,10 +705,16 @@ __global__ void __launch_bounds__(512)
       for (int j = 0; j < 4; ++j) c[4 * g + j] = v[j];
     }
     f32x4v cur[4], nxt[4];
+    f32x4v pcur[ST ? 4 : 1], pnxt[ST ? 4 : 1];  // ST: L_pq streamed too
     if (p > 0) {
       const f32x4v* L0 = reinterpret_cast<const f32x4v*>(gtile(I, 0) + lo * 32 + 16 * hi);
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = L0[j];
+      if constexpr (ST) {
+        const f32x4v* P0 = reinterpret_cast<const f32x4v*>(gtile(p, 0) + lo * 32 + 16 * hi);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pcur[j] = P0[j];
+      }
     }
 #pragma unroll 1
     for (int q = 0; q < p; ++q) {
@@ -711,22 +722,36 @@ __global__ void __launch_bounds__(512)
         const f32x4v* Ln = reinterpret_cast<const f32x4v*>(gtile(I, q + 1) + lo * 32 + 16 * hi);
 #pragma unroll
         for (int j = 0; j < 4; ++j) nxt[j] = Ln[j];
-      }
-      const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+        if constexpr (ST) {
+          const f32x4v* Pn = reinterpret_cast<const f32x4v*>(gtile(p, q + 1) + lo * 32 + 16 * hi);
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
+          for (int j = 0; j < 4; ++j) pnxt[j] = Pn[j];
+        }
+      }
+      if constexpr (ST) {
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2)
+          c = mfma32(-pcur[s2 >> 2][s2 & 3], cur[s2 >> 2][s2 & 3], c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pcur[j] = pnxt[j];
+      } else {
+        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
     }
     return c;
   };
+  static_assert(!ST || RD, "streamed operands need the right-looking diagonals");
 
 #pragma unroll 1
   for (int p = 0; p < T; ++p) {
     // ---- A: row p of L (the thread's loads issued four at a time, each
     // unconditional -- past the row it re-reads tile (p, 0) and drops it --
     // so a panel costs two HBM round trips, not one per float4) ----
-    {
+    if constexpr (!ST) {
       constexpr int NA = ((T - 1) * 256 + 511) / 512, NB = 4;
       const int n = p * 256;
 #pragma unroll
@@ -754,8 +779,8 @@ __global__ void __launch_bounds__(512)
           }
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
     // ---- B ----
     f32x16 acc0;
     if (wave == 0) {
@@ -796,10 +821,19 @@ __global__ void __launch_bounds__(512)
         float r = 0.0f;
 #pragma unroll 1
         for (int q = 0; q < p; ++q) {  // row lo of L_pq . y_q, k halves by hi
-          const float* L = rowL + q * LP + lo * 33 + 16 * hi;
           const float* y = yv + 32 * q + 16 * hi;
+          if constexpr (ST) {
+            const f32x4v* Lg = reinterpret_cast<const f32x4v*>(gtile(p, q) + lo * 32 + 16 * hi);
+            f32x4v lv[4];
 #pragma unroll
-          for (int k2 = 0; k2 < 16; ++k2) r = __builtin_fmaf(L[k2], y[k2], r);
+            for (int j = 0; j < 4; ++j) lv[j] = Lg[j];
+#pragma unroll
+            for (int k2 = 0; k2 < 16; ++k2) r = __builtin_fmaf(lv[k2 >> 2][k2 & 3], y[k2], r);
+          } else {
+            const float* L = rowL + q * LP + lo * 33 + 16 * hi;
+#pragma unroll
+            for (int k2 = 0; k2 < 16; ++k2) r = __builtin_fmaf(L[k2], y[k2], r);
+          }
         }
         r += __shfl_xor(r, 32);
         if (hi == 0) rv[lo] = yv[32 * p + lo] - r;
@@ -1481,6 +1515,14 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(512));
     if (err == hipSuccess)
+      err = hipFuncSetAttribute((const void*)wide_chol_kernel<16, true, 2, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)wide_chol_lds_bytes(512));
+    if (err == hipSuccess)
+      err = hipFuncSetAttribute(
+          (const void*)wide_chol_kernel<16, true, FRECSYS_WIDE_CHOL_WPE, false, true>,
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_chol_lds_bytes(512));
+    if (err == hipSuccess)
       err = hipFuncSetAttribute((const void*)wide_chol_kernel<32>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(1024));
@@ -1518,6 +1560,12 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
     else if (Dp == 512 && wide_chol_rd() == 2)
       hipLaunchKernelGGL((wide_chol_kernel<16, true, 2, true>), dim3((unsigned)nb), dim3(512),
                          wide_chol_lds_bytes(Dp), s, a, s0, ws);
+    else if (Dp == 512 && wide_chol_rd() == 3)
+      hipLaunchKernelGGL((wide_chol_kernel<16, true, 2, true, true>), dim3((unsigned)nb),
+                         dim3(512), wide_chol_lds_bytes(Dp), s, a, s0, ws);
+    else if (Dp == 512 && wide_chol_rd() == 4)
+      hipLaunchKernelGGL((wide_chol_kernel<16, true, FRECSYS_WIDE_CHOL_WPE, false, true>),
+                         dim3((unsigned)nb), dim3(512), wide_chol_lds_bytes(Dp), s, a, s0, ws);
     else if (Dp == 512 && wide_chol_rd())
       hipLaunchKernelGGL((wide_chol_kernel<16, true>), dim3((unsigned)nb), dim3(512),
                          wide_chol_lds_bytes(Dp), s, a, s0, ws);
