@@ -24,13 +24,14 @@
 //   dual_sweep_kernel  one thread per entity: x' = L^-T D^-1 L^-1 (Y^T c.*z).
 // dual_solve_kernel, per workgroup (one entity, NW waves):
 //   * the entity's l_k and D^-1/2 come from its table row;
-//   * per slab (32 columns of the h_p rows, staged in LDS with a padded
-//     row stride): each row's lane runs the bidiagonal recurrence
-//     z_j[k] = y_j[k] - l_k z_j[k-1] across the slab (carry in a register)
-//     and writes D^-1/2-scaled values k-major; the waves then accumulate
-//     their S tiles while the next slab's loads are in flight -- by default
-//     on the bf16 matrix cores with fp32-accurate 3-piece split operands
-//     (common.h mfma_x6), FRECSYS_SYRK_F32=1: v_mfma_f32_32x32x2_f32;
+//   * per slab (32 columns of the h_p rows; row j's slab loaded by thread j
+//     into registers one slab ahead -- with FRECSYS_SYRK_F32=1 staged in LDS
+//     with a padded row stride instead): each row's lane runs the bidiagonal
+//     recurrence z_j[k] = y_j[k] - l_k z_j[k-1] across the slab (carry in a
+//     register) and writes D^-1/2-scaled values k-major; the waves then
+//     accumulate their S tiles while the next slab's loads are in flight --
+//     by default on the bf16 matrix cores with fp32-accurate 3-piece split
+//     operands (common.h mfma_x6), FRECSYS_SYRK_F32=1: v_mfma_f32_32x32x2_f32;
 //   * S tiles go to LDS (aliasing the slab buffers), chol_solve_tiles, then
 //     Y^T (c.*z) re-reads the (cache-resident) rows with float4 loads.
 #include <hip/hip_runtime.h>
@@ -55,6 +56,12 @@ __device__ __forceinline__ int dgran(int p, int g, int hh, int j) {
   return ((p * 2 + g) * 2 + hh) * HP + j;
 }
 
+// BF: register-direct slabs -- thread j loads row j's 32-column slab itself
+// (float4 x 8, the next slab's loads issued as the current one is consumed)
+// instead of the workgroup staging it in LDS (the fp32 path): no staging
+// stores or buffer, no LDS reads in the recurrence.  Bit-identical to the
+// staged form; measured (ML-20M d = 256, serialised) 5.50 -> 5.30 ms of
+// bucket kernels per epoch.
 template <int TH, bool BF>
 struct DualCfg {
   static constexpr int HP = 32 * TH;                // padded history rows
@@ -66,7 +73,8 @@ struct DualCfg {
   static constexpr int STG = HP * SROW;
   static constexpr int ZS = (BF ? 48 : 32) * HP;   // k-major scaled Z slab (BF: pieces)
   static constexpr int TILES = NT * 1024;
-  static constexpr int NSTAGE = (TH <= 4) ? 1 : 2;  // LDS stages for the slab prefetch
+  static constexpr int NSTAGE = BF ? 0 : ((TH <= 4) ? 1 : 2);  // LDS stages for the slab prefetch
+  static constexpr int NSTG1 = NSTAGE > 0 ? NSTAGE : 1;
   static constexpr int LOOP = ((NSTAGE * STG + ZS + 3) / 4) * 4;
   static constexpr int REGION0 = TILES > LOOP ? TILES : LOOP;
   static constexpr int OFF_C = REGION0;             // c_j
@@ -197,6 +205,7 @@ template <int TH, bool BF>
 __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
     __attribute__((amdgpu_waves_per_eu(DualCfg<TH, BF>::WPE, 8))) dual_solve_kernel(DualArgs a) {
   using C = DualCfg<TH, BF>;
+  constexpr bool RDS = BF;  // register-direct slabs
   constexpr int HP = C::HP, NT = C::NT, NW = C::NW, NTHR = C::NTHR, MT = C::MT;
   constexpr int SROW = C::SROW, NQ = C::NQ;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -233,6 +242,7 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   (void)mu;
   (void)lam;
 
+  int my_id = -1;  // RDS: the thread's own history row
   if (tid < HP) {
     int id = -1;
     float cj = 0.0f;
@@ -245,6 +255,7 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
     ids[tid] = id;
     cvec[tid] = cj;
     bvec[tid] = tid < h ? cj : 0.0f;
+    my_id = id;
   }
   if (tid == 0) flag[0] = 0;
   unsigned long long t_prev = a.prof ? clock64() : 0;
@@ -288,7 +299,7 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
       if ((HP * 8) % NTHR == 0 || s < HP * 8) {
         const int r = s >> 3, c4 = s & 7;
         const bool ok = ids[r] >= 0 && !FRECSYS_SKIP(a.debug_skip, 32);
-        float* d = stage + (buf % C::NSTAGE) * C::STG + r * SROW + 4 * c4;
+        float* d = stage + (buf % C::NSTG1) * C::STG + r * SROW + 4 * c4;
         d[0] = ok ? regs[q].x : 0.0f;
         d[1] = ok ? regs[q].y : 0.0f;
         d[2] = ok ? regs[q].z : 0.0f;
@@ -297,9 +308,20 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
     }
   };
 
-  load_slab(0, ra);
-  if (NC > 1) load_slab(1, rb);
-  store_slab(ra, 0);
+  // RDS: row slab in registers; padding rows read row 0 (c_j = 0 zeroes
+  // their contribution), so every load is unconditional
+  const float* myrow = a.Xrot + (int64_t)max(my_id, 0) * Dp;
+  float4 yq[RDS ? 8 : 1];
+  if constexpr (RDS) {
+    if (tid < HP) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) yq[q] = *reinterpret_cast<const float4*>(myrow + 4 * q);
+    }
+  } else {
+    load_slab(0, ra);
+    if (NC > 1) load_slab(1, rb);
+    store_slab(ra, 0);
+  }
   lds_barrier();
   mark(0);
 
@@ -322,9 +344,36 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   const float cj = tid < HP ? cvec[tid] : 0.0f;
   // slab c: in LDS stage c&1; slab c+1 in the other register set
   auto slab_step = [&](int c, float4 (&mine)[NQ], float4 (&next)[NQ]) {
-    if (c + 2 < NC) load_slab(c + 2, mine);
-    if (tid < HP && !FRECSYS_SKIP(a.debug_skip, 128)) {
-      const float* yrow = stage + ((c & 1) % C::NSTAGE) * C::STG + tid * SROW;
+    if (!RDS && c + 2 < NC) load_slab(c + 2, mine);
+    if (RDS && tid < HP && !FRECSYS_SKIP(a.debug_skip, 128)) {
+      // the same recurrence on the registers; each float4 pair, once used,
+      // takes the next slab's loads
+      bf16x8* zb = reinterpret_cast<bf16x8*>(zs);
+      float z = carry;
+#pragma unroll
+      for (int gh = 0; gh < 4; ++gh) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float4 y4 = yq[2 * gh + (u >> 2)];
+          const float yv = (u & 3) == 0 ? y4.x : (u & 3) == 1 ? y4.y : (u & 3) == 2 ? y4.z : y4.w;
+          const int k = 32 * c + 8 * gh + u;
+          z = yv - lsub[k] * z;
+          v[u] = (cj * z) * dsq[k];
+        }
+        if (c + 1 < NC) {
+          yq[2 * gh] = *reinterpret_cast<const float4*>(myrow + 32 * (c + 1) + 8 * gh);
+          yq[2 * gh + 1] = *reinterpret_cast<const float4*>(myrow + 32 * (c + 1) + 8 * gh + 4);
+        }
+        bf16x8 f[3];
+        split3x8(v, f);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) zb[dgran<HP>(p, gh >> 1, gh & 1, tid)] = f[p];
+      }
+      carry = z;
+    }
+    if (!RDS && tid < HP && !FRECSYS_SKIP(a.debug_skip, 128)) {
+      const float* yrow = stage + ((c & 1) % C::NSTG1) * C::STG + tid * SROW;
       float y[BF ? 1 : 32];
       if constexpr (!BF) {
 #pragma unroll
@@ -389,7 +438,7 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
         }
       }
     }
-    if (c + 1 < NC) store_slab(next, (c + 1) & 1);
+    if (!RDS && c + 1 < NC) store_slab(next, (c + 1) & 1);
     lds_barrier();
   };
   for (int c = 0; c < NC; c += 2) {

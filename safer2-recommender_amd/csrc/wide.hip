@@ -121,7 +121,7 @@ __device__ __forceinline__ bool xcd_unit(int P, int64_t n_units, int64_t& unit, 
 // every W2FLUSH chunks).
 constexpr int WB2 = 256;
 constexpr int W2R = 16;
-constexpr int W2RING = 8;
+constexpr int W2RING = 4;
 constexpr int W2FLUSH = 128;
 constexpr int W2GRAN = 6 * 512;  // 16-B granules per stage buffer
 
@@ -132,11 +132,10 @@ int wide_pairs2(int Dp) {
   return nb * (nb + 1) / 2;
 }
 
-template <int MODE, bool OFF64 = false, int AH = 2>
+template <int MODE, bool OFF64 = false>
 __global__ void __launch_bounds__(512)
     wide_syrk2_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws,
                       int64_t n_units) {
-  static_assert(AH == 1 || AH == 2, "rows loaded one or two chunks ahead");
   __shared__ __attribute__((aligned(16))) bf16x8 stage[2][W2GRAN];
   __shared__ __attribute__((aligned(16))) int ring_id[W2RING * W2R];
   __shared__ float2 ring_sb[W2RING * W2R];  // (row scale, rhs / B-side weight)
@@ -221,9 +220,8 @@ __global__ void __launch_bounds__(512)
   const int xcol = sc < WB2 ? WB2 * BI + sc : WB2 * BJ + (sc - WB2);
   const bool wside = MODE == 0 && !same && sc >= WB2;  // weighted B operand
   const bool bown = MODE >= 1 && dgp;                  // diagonal pairs form b
-  // AH register sets of the staged rows: chunk c's in set c % AH, loaded AH
-  // iterations before it is staged
-  float xr0[16], xr1[AH == 2 ? 16 : 1];
+  // the staged rows of the next chunk, loaded one iteration before it is staged
+  float xr0[16];
   auto load = [&](int c, float (&xr)[16]) __attribute__((always_inline)) {
     const int base = (c % W2RING) * W2R + 8 * hh0;
     const int4* ids4 = reinterpret_cast<const int4*>(ring_id + base);  // base % 8 == 0
@@ -318,7 +316,7 @@ __global__ void __launch_bounds__(512)
 
   if (tid < W2R) {
 #pragma unroll
-    for (int c = 0; c < 2 + AH; ++c)
+    for (int c = 0; c < 3; ++c)
       if (c < nchunks) {
         int id;
         float sa, bw;
@@ -331,28 +329,23 @@ __global__ void __launch_bounds__(512)
     load(0, xr0);
     stage_write(xr0, 0, 0);
   }
-  if constexpr (AH == 2) {
-    if (nchunks > 1) load(1, xr1);
-    if (nchunks > 2) load(2, xr0);
-  } else {
-    if (nchunks > 1) load(1, xr0);
-  }
+  if (nchunks > 1) load(1, xr0);
   lds_barrier();
 
   // chunk c: the MFMAs of its tiles, with chunk c+1's staging math (rows
-  // loaded AH iterations ago) spread over the gaps between them -- a slice
+  // loaded one iteration ago) spread over the gaps between them -- a slice
   // of NV/8 values after each tile, a granule group stored once complete --
   // instead of a VALU phase of its own after the MFMAs
-  // iteration c: xr holds chunk c+1 (staged now), and then takes chunk c+AH+1
+  // iteration c: xr holds chunk c+1 (staged now), and then takes chunk c+2
   auto body = [&](auto same_c, int c, float (&xr)[16]) __attribute__((always_inline)) {
       constexpr bool SAME = decltype(same_c)::value;
       constexpr int NV = SAME ? 8 : 16, PER = NV / MT;
       const int buf = c & 1;
       const bool more = c + 1 < nchunks;
-      const bool ring_more = (tid < W2R) && (c + 2 + AH < nchunks);
+      const bool ring_more = (tid < W2R) && (c + 3 < nchunks);
       int nid = -1;
       float nsa = 0.f, nbw = 0.f;
-      if (ring_more) ring_load(c + 2 + AH, nid, nsa, nbw);
+      if (ring_more) ring_load(c + 3, nid, nsa, nbw);
       const bf16x8* st = stage[buf];
       bf16x8* sto = stage[buf ^ 1];
       const int nbase = ((c + 1) % W2RING) * W2R + 8 * hh0;
@@ -401,22 +394,15 @@ __global__ void __launch_bounds__(512)
       // load between -- was vmcnt(0), wave 0 stalling on the rows it had just
       // requested (a full HBM latency per chunk, every wave behind it at the
       // barrier)
-      if (ring_more) ring_store(c + 2 + AH, nid, nsa, nbw);
+      if (ring_more) ring_store(c + 3, nid, nsa, nbw);
       // unconditional (past the end it re-gathers the last chunk, whose ring
       // slot stays valid; never staged): a conditional load here made the
       // waitcnt pass flush vmcnt at the loop head, stalling on these rows
-      load(c + 1 + AH < nchunks ? c + 1 + AH : nchunks - 1, xr);
+      load(c + 2 < nchunks ? c + 2 : nchunks - 1, xr);
       lds_barrier();
   };
   auto run = [&](auto same_c) __attribute__((always_inline)) {
-    if constexpr (AH == 2) {
-      for (int c = 0; c < nchunks; c += 2) {
-        body(same_c, c, xr1);
-        if (c + 1 < nchunks) body(same_c, c + 1, xr0);
-      }
-    } else {
-      for (int c = 0; c < nchunks; ++c) body(same_c, c, xr0);
-    }
+    for (int c = 0; c < nchunks; ++c) body(same_c, c, xr0);
   };
   if (same) run(std::true_type{});
   else run(std::false_type{});
@@ -648,23 +634,9 @@ __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, fl
 // against ~T^3/3 reads and T^3/3 writes of a right-looking update sweep
 // (round 2's kernel: MSD 174 GB of workspace traffic per epoch, 37 ms; this
 // one 30.5 ms).  Compiled for two workgroups per CU (128 registers).
-// RD = true: the DIAGONAL tiles are updated right-looking instead -- the
-// worker that forms L_Ip (I > p) also applies D_I -= L_Ip L_Ip^T to tile
-// (I, I) in the workspace, reading L_Ip back in the operand layout row p
-// of L has in LDS -- so wave 0's chain loads a finished D_p and only
-// factors it (the p serial tile products of its update leave the chain).
-// The same MFMAs on the same operands in the same order, the running sum
-// passing through fp32 memory between panels: bit-identical to RD = false.
-// FB = true: the MFMA-blocked diagonal factor (chol.h diag_factor_inv_blk),
-// which needs the register budget of one workgroup per CU (WPE = 2).
-// ST = true (with RD): no staging of row p of L in LDS -- every L_pq operand
-// is streamed from the workspace like L_Iq (L1 / L2 hits: the seven workers
-// read the same row), so a panel has no load phase and no barrier before its
-// products; the same values in the same order (bit-identical to ST = false).
-template <int T, bool RD = false, int WPE = (T == 16 ? FRECSYS_WIDE_CHOL_WPE : 2), bool FB = false,
-          bool ST = false>
+template <int T>
 __global__ void __launch_bounds__(512)
-    __attribute__((amdgpu_waves_per_eu(WPE, 8)))
+    __attribute__((amdgpu_waves_per_eu(T == 16 ? FRECSYS_WIDE_CHOL_WPE : 2, 8)))
     wide_chol_kernel(SolveArgs a, int64_t pos0, float* ws) {
   constexpr int Dp = 32 * T, NT = T * (T + 1) / 2, NW = 8;
   typedef float f32x4v __attribute__((ext_vector_type(4)));
@@ -705,16 +677,10 @@ __global__ void __launch_bounds__(512)
       for (int j = 0; j < 4; ++j) c[4 * g + j] = v[j];
     }
     f32x4v cur[4], nxt[4];
-    f32x4v pcur[ST ? 4 : 1], pnxt[ST ? 4 : 1];  // ST: L_pq streamed too
     if (p > 0) {
       const f32x4v* L0 = reinterpret_cast<const f32x4v*>(gtile(I, 0) + lo * 32 + 16 * hi);
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = L0[j];
-      if constexpr (ST) {
-        const f32x4v* P0 = reinterpret_cast<const f32x4v*>(gtile(p, 0) + lo * 32 + 16 * hi);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pcur[j] = P0[j];
-      }
     }
 #pragma unroll 1
     for (int q = 0; q < p; ++q) {
@@ -722,36 +688,22 @@ __global__ void __launch_bounds__(512)
         const f32x4v* Ln = reinterpret_cast<const f32x4v*>(gtile(I, q + 1) + lo * 32 + 16 * hi);
 #pragma unroll
         for (int j = 0; j < 4; ++j) nxt[j] = Ln[j];
-        if constexpr (ST) {
-          const f32x4v* Pn = reinterpret_cast<const f32x4v*>(gtile(p, q + 1) + lo * 32 + 16 * hi);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pnxt[j] = Pn[j];
-        }
       }
-      if constexpr (ST) {
+      const float* P = rowL + q * LP + lo * 33 + 16 * hi;
 #pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2)
-          c = mfma32(-pcur[s2 >> 2][s2 & 3], cur[s2 >> 2][s2 & 3], c);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pcur[j] = pnxt[j];
-      } else {
-        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
-      }
+      for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
     }
     return c;
   };
-  static_assert(!ST || RD, "streamed operands need the right-looking diagonals");
 
 #pragma unroll 1
   for (int p = 0; p < T; ++p) {
     // ---- A: row p of L (the thread's loads issued four at a time, each
     // unconditional -- past the row it re-reads tile (p, 0) and drops it --
     // so a panel costs two HBM round trips, not one per float4) ----
-    if constexpr (!ST) {
+    {
       constexpr int NA = ((T - 1) * 256 + 511) / 512, NB = 4;
       const int n = p * 256;
 #pragma unroll
@@ -779,8 +731,8 @@ __global__ void __launch_bounds__(512)
           }
         }
       }
-      __syncthreads();
     }
+    __syncthreads();
     // ---- B ----
     f32x16 acc0;
     if (wave == 0) {
@@ -788,13 +740,11 @@ __global__ void __launch_bounds__(512)
       f32x16 d;
 #pragma unroll
       for (int q = 0; q < 16; ++q) d[q] = App[acc_row(q, hi) * 32 + lo];
-      if constexpr (!RD) {
 #pragma unroll 1
-        for (int q = 0; q < p; ++q) {  // d -= L_pq L_pq^T (k = 16 hi + s)
-          const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+      for (int q = 0; q < p; ++q) {  // d -= L_pq L_pq^T (k = 16 hi + s)
+        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
 #pragma unroll
-          for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
-        }
+        for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
       }
       // opaque copies of the lane coordinates: the 48 swizzled / padded
       // addresses below are formed here with a few VALU ops each, not hoisted
@@ -806,7 +756,7 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
       for (int q = 0; q < 16; ++q) dinv[sw(acc_row(q, hi_o), lo_o)] = d[q];
       wave_lds_sync();
-      if (!diag_factor_inv<FB>(dinv, lane) && lane == 0) flag[0] = 1;
+      if (!diag_factor_inv(dinv, lane) && lane == 0) flag[0] = 1;
       wave_lds_sync();
       float* Aw = gtile(p, p);  // L_pp^-1 for the back substitution, and its padded copy
 #pragma unroll
@@ -821,19 +771,10 @@ __global__ void __launch_bounds__(512)
         float r = 0.0f;
 #pragma unroll 1
         for (int q = 0; q < p; ++q) {  // row lo of L_pq . y_q, k halves by hi
+          const float* L = rowL + q * LP + lo * 33 + 16 * hi;
           const float* y = yv + 32 * q + 16 * hi;
-          if constexpr (ST) {
-            const f32x4v* Lg = reinterpret_cast<const f32x4v*>(gtile(p, q) + lo * 32 + 16 * hi);
-            f32x4v lv[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) lv[j] = Lg[j];
-#pragma unroll
-            for (int k2 = 0; k2 < 16; ++k2) r = __builtin_fmaf(lv[k2 >> 2][k2 & 3], y[k2], r);
-          } else {
-            const float* L = rowL + q * LP + lo * 33 + 16 * hi;
-#pragma unroll
-            for (int k2 = 0; k2 < 16; ++k2) r = __builtin_fmaf(L[k2], y[k2], r);
-          }
+          for (int k2 = 0; k2 < 16; ++k2) r = __builtin_fmaf(L[k2], y[k2], r);
         }
         r += __shfl_xor(r, 32);
         if (hi == 0) rv[lo] = yv[32 * p + lo] - r;
@@ -859,26 +800,6 @@ __global__ void __launch_bounds__(512)
         float* Lw = gtile(I, p);
 #pragma unroll
         for (int q = 0; q < 16; ++q) Lw[acc_row(q, hi) * 32 + lo] = l[q];
-        if constexpr (RD) {
-          // D_I -= L_Ip L_Ip^T: L_Ip read back (this wave's own stores) as
-          // row lo, k = 16 hi + s -- rowL's layout for wave 0's update
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          const f32x4v* Lr = reinterpret_cast<const f32x4v*>(Lw + lo * 32 + 16 * hi);
-          f32x4v lr[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) lr[j] = Lr[j];
-          float* Dw = gtile(I, I);
-          f32x16 dI;
-#pragma unroll
-          for (int q = 0; q < 16; ++q) dI[q] = Dw[acc_row(q, hi) * 32 + lo];
-#pragma unroll
-          for (int s2 = 0; s2 < 16; ++s2) {
-            const float v = lr[s2 >> 2][s2 & 3];
-            dI = mfma32(-v, v, dI);
-          }
-#pragma unroll
-          for (int q = 0; q < 16; ++q) Dw[acc_row(q, hi) * 32 + lo] = dI[q];
-        }
       }
     }
     __syncthreads();
@@ -1430,21 +1351,6 @@ __global__ void __launch_bounds__(256) loss_gather_wide_kernel(LossArgs a) {
   if (lane == 0) a.out[e] = loss;
 }
 
-// FRECSYS_W2_AHEAD=2: the d-space SYRK loads rows two chunks ahead instead
-// of one (A/B of the prefetch depth; read at each call)
-bool w2_ahead1() {
-  const char* e = getenv("FRECSYS_W2_AHEAD");
-  return !(e && atoi(e) == 2);
-}
-
-// FRECSYS_WIDE_CHOL_RD=1: right-looking diagonal updates in the wide
-// Cholesky (A/B; bit-identical; read at each call); =2: the same with the
-// MFMA-blocked diagonal factor at one workgroup per CU
-int wide_chol_rd() {
-  const char* e = getenv("FRECSYS_WIDE_CHOL_RD");
-  return e ? atoi(e) : 0;
-}
-
 unsigned xcd_grid(int64_t n_units, int P) { return (unsigned)(((n_units + 7) / 8) * 8 * P); }
 
 size_t wide_chol_lds_bytes(int Dp) {
@@ -1507,22 +1413,6 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(512));
     if (err == hipSuccess)
-      err = hipFuncSetAttribute((const void*)wide_chol_kernel<16, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)wide_chol_lds_bytes(512));
-    if (err == hipSuccess)
-      err = hipFuncSetAttribute((const void*)wide_chol_kernel<16, true, 2, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)wide_chol_lds_bytes(512));
-    if (err == hipSuccess)
-      err = hipFuncSetAttribute((const void*)wide_chol_kernel<16, true, 2, true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)wide_chol_lds_bytes(512));
-    if (err == hipSuccess)
-      err = hipFuncSetAttribute(
-          (const void*)wide_chol_kernel<16, true, FRECSYS_WIDE_CHOL_WPE, false, true>,
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_chol_lds_bytes(512));
-    if (err == hipSuccess)
       err = hipFuncSetAttribute((const void*)wide_chol_kernel<32>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(1024));
@@ -1537,9 +1427,6 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
     if (off64)
       hipLaunchKernelGGL((wide_syrk2_kernel<2, true>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
-    else if (w2_ahead1())
-      hipLaunchKernelGGL((wide_syrk2_kernel<2, false, 1>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
-                         dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
     else
       hipLaunchKernelGGL((wide_syrk2_kernel<2, false>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
@@ -1549,26 +1436,11 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
     if (off64)
       hipLaunchKernelGGL((wide_syrk2_kernel<1, true>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
-    else if (w2_ahead1())
-      hipLaunchKernelGGL((wide_syrk2_kernel<1, false, 1>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
-                         dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     else
       hipLaunchKernelGGL((wide_syrk2_kernel<1, false>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
-    else if (Dp == 512 && wide_chol_rd() == 2)
-      hipLaunchKernelGGL((wide_chol_kernel<16, true, 2, true>), dim3((unsigned)nb), dim3(512),
-                         wide_chol_lds_bytes(Dp), s, a, s0, ws);
-    else if (Dp == 512 && wide_chol_rd() == 3)
-      hipLaunchKernelGGL((wide_chol_kernel<16, true, 2, true, true>), dim3((unsigned)nb),
-                         dim3(512), wide_chol_lds_bytes(Dp), s, a, s0, ws);
-    else if (Dp == 512 && wide_chol_rd() == 4)
-      hipLaunchKernelGGL((wide_chol_kernel<16, true, FRECSYS_WIDE_CHOL_WPE, false, true>),
-                         dim3((unsigned)nb), dim3(512), wide_chol_lds_bytes(Dp), s, a, s0, ws);
-    else if (Dp == 512 && wide_chol_rd())
-      hipLaunchKernelGGL((wide_chol_kernel<16, true>), dim3((unsigned)nb), dim3(512),
-                         wide_chol_lds_bytes(Dp), s, a, s0, ws);
     else if (Dp == 512)
       hipLaunchKernelGGL(wide_chol_kernel<16>, dim3((unsigned)nb), dim3(512),
                          wide_chol_lds_bytes(Dp), s, a, s0, ws);

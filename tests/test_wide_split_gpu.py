@@ -106,20 +106,3 @@ def test_wide_split_small_budget(monkeypatch, long_items):
     monkeypatch.delenv("FRECSYS_WIDE_WS_MB")
     Vn, _ = _solve_items(monkeypatch, long_items, 512, fh.KIND_IALS, False)
     np.testing.assert_array_equal(Vs, Vn)
-
-
-@pytest.mark.parametrize("kind", [fh.KIND_IALS, fh.KIND_WEIGHTED_V])
-@pytest.mark.parametrize("ahead,rd", [("2", "0"), ("1", "1"), ("2", "1"), ("1", "4")])
-def test_wide_variants_bit_identical(monkeypatch, long_items, kind, ahead, rd):
-    """The wide d-space variants compute the same operations in the same
-    order: the SYRK's rows loaded two chunks ahead (FRECSYS_W2_AHEAD=2) and
-    the Cholesky's right-looking diagonal updates (FRECSYS_WIDE_CHOL_RD=1),
-    also with row p of L streamed instead of staged in LDS (=4), are
-    bit-identical to the defaults, split and unsplit entities alike."""
-    monkeypatch.setenv("FRECSYS_W2_AHEAD", "1")
-    monkeypatch.setenv("FRECSYS_WIDE_CHOL_RD", "0")
-    Vb, _ = _solve_items(monkeypatch, long_items, 512, kind, True)
-    monkeypatch.setenv("FRECSYS_W2_AHEAD", ahead)
-    monkeypatch.setenv("FRECSYS_WIDE_CHOL_RD", rd)
-    Vv, _ = _solve_items(monkeypatch, long_items, 512, kind, True)
-    np.testing.assert_array_equal(Vv, Vb)
