@@ -68,3 +68,13 @@ $(ABL_LIB): $(HIP_SRCS) $(HDRS)
 	@mkdir -p ab/obj
 	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) -DFRECSYS_ABLATION -c $$f -o ab/obj/$$(basename $$f .hip).o || exit 1; done
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ ab/obj/*.o -lrccl
+
+# A/B build of the library with extra defines, for a timed comparison on the
+# GPU box (a copy over frecsys_hip/libfrecsys_hip.so swaps it in there), e.g.
+#   make abvar ABDEF=-DFRECSYS_CHOL_X6=1 ABNAME=x6  ->  ab/libfrecsys_hip_x6.so
+ABNAME ?= var
+.PHONY: abvar
+abvar: $(HIP_SRCS) $(HDRS)
+	@mkdir -p ab/obj/$(ABNAME)
+	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) $(ABDEF) -c $$f -o ab/obj/$(ABNAME)/$$(basename $$f .hip).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o ab/libfrecsys_hip_$(ABNAME).so ab/obj/$(ABNAME)/*.o -lrccl

@@ -14,6 +14,12 @@
 #ifndef FRECSYS_DIAG_BLK
 #define FRECSYS_DIAG_BLK 1
 #endif
+// 1: the dataflow Cholesky's TRSM and trailing-update tile products on the
+// bf16 matrix cores with 3-piece split operands (tile_pqT_x6), in the kernels
+// that run the blocked diagonal factor (BLK: the register budget for it).
+#ifndef FRECSYS_CHOL_X6
+#define FRECSYS_CHOL_X6 1
+#endif
 
 namespace frecsys_hip {
 
@@ -234,6 +240,34 @@ __device__ __forceinline__ f32x16 tile_pqT(const float* P, const float* Q, int l
   return u;
 }
 
+// The same product with fp32-accurate split operands (common.h mfma_x6):
+// lane (lo, hi) takes k = 16 g + 8 hi + j of row lo of P and of Q, splits
+// them into three bf16 pieces in registers, and 2 x 6 v_mfma_f32_32x32x16_bf16
+// (32 cycles each) replace 16 v_mfma_f32_32x32x2_f32 (64 cycles each).
+// SAME: P == Q (one operand split, used on both sides).
+template <bool SAME = false>
+__device__ __forceinline__ f32x16 tile_pqT_x6(const float* P, const float* Q, int lo, int hi) {
+  f32x16 u = f32x16{0.f};
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float pv[8], qv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      pv[j] = P[sw(lo, 16 * g + 8 * hi + j)];
+      if (!SAME) qv[j] = Q[sw(lo, 16 * g + 8 * hi + j)];
+    }
+    bf16x8 pf[3], qf[3];
+    split3x8(pv, pf);
+    if (SAME) {
+      u = mfma_x6(pf, pf, u);
+    } else {
+      split3x8(qv, qf);
+      u = mfma_x6(pf, qf, u);
+    }
+  }
+  return u;
+}
+
 // ---------------------------------------------------------------------
 // Solve A x = b for the SPD matrix whose lower T(T+1)/2 tiles sit in LDS
 // (tile (I, J) at tiles + tidx(I, J) * 1024, swizzled), NW waves.
@@ -417,6 +451,8 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
                                               unsigned long long* prof = nullptr) {
   static_assert(NW >= 2, "one chain wave and at least one worker");
   constexpr int NT = T * (T + 1) / 2;
+  // split-bf16 tile products where the register budget allows (as BLK)
+  constexpr bool X6 = FRECSYS_CHOL_X6 && BLK;
   const unsigned long long t0 = prof ? clock64() : 0;
   const int lane = tid & 63, lo = lane & 31, hi = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -432,7 +468,8 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   auto trsm = [&](int I, int p) {  // S(I, p)
     float* Aip = tiles + tidx(I, p) * 1024;
     if (!FRECSYS_SKIP(debug_skip, 4)) {
-      const f32x16 u = tile_pqT(Aip, tiles + tidx(p, p) * 1024, lo, hi);
+      const f32x16 u = X6 ? tile_pqT_x6(Aip, tiles + tidx(p, p) * 1024, lo, hi)
+                          : tile_pqT(Aip, tiles + tidx(p, p) * 1024, lo, hi);
 #pragma unroll
       for (int q = 0; q < 16; ++q) Aip[sw(acc_row(q, hi), lo)] = u[q];
     }
@@ -447,7 +484,11 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   auto update = [&](int I, int J, int p) {  // U(I, J, p)
     float* Aij = tiles + tidx(I, J) * 1024;
     if (!FRECSYS_SKIP(debug_skip, 8)) {
-      const f32x16 u = tile_pqT(tiles + tidx(I, p) * 1024, tiles + tidx(J, p) * 1024, lo, hi);
+      const float* Li = tiles + tidx(I, p) * 1024;
+      const float* Lj = tiles + tidx(J, p) * 1024;
+      const f32x16 u = !X6     ? tile_pqT(Li, Lj, lo, hi)
+                       : I == J ? tile_pqT_x6<true>(Li, Li, lo, hi)
+                                : tile_pqT_x6(Li, Lj, lo, hi);
 #pragma unroll
       for (int q = 0; q < 16; ++q) Aij[sw(acc_row(q, hi), lo)] -= u[q];
     }
