@@ -1394,9 +1394,13 @@ namespace {
 // The d-space solve of the queue prefix ap.order[0..ap.n_rows): the tiled
 // one-workgroup-per-entity kernels (long histories split) up to Dp = 256,
 // the HBM-workspace batches of wide.hip at Dp = 512 / 1024.
+// aux (Dp <= 256, optional): an idle stream for the long histories' slabs
+// and then their entities' solves, so the slabs run beside the other
+// entities' solve instead of before it (s waits for aux at the end).
 int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
                   const std::function<int64_t(int64_t)>& heff, hipStream_t s,
-                  const std::string& pre, bool can_split, int side, bool vq) {
+                  const std::string& pre, bool can_split, int side, bool vq,
+                  hipStream_t aux = nullptr) {
   if (wide_dim(c->Dp)) {
     const size_t slot = wide_slot_floats(c->Dp);
     const int64_t budget = (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (slot * sizeof(float)));
@@ -1425,7 +1429,16 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
                         INT64_MAX, s);
     if (rc) return rc;
   }
-  if (ap.n_work > 0) {
+  const bool side_split = ap.n_work > 0 && aux != nullptr;
+  if (side_split) {
+    // slabs, then the split entities' solves (they start from the slabs) on
+    // aux; the other entities on s meanwhile
+    HIP_TRY(c, hipEventRecord(c->ev_fork, s));
+    HIP_TRY(c, hipStreamWaitEvent(aux, c->ev_fork, 0));
+    const size_t k = ktimer_begin(c, pre + ".split", aux);
+    HIP_TRY(c, launch_split_syrk(c->Dp, ap, aux));
+    ktimer_end(c, k, aux);
+  } else if (ap.n_work > 0) {
     const size_t k = ktimer_begin(c, pre + ".split", s);
     HIP_TRY(c, launch_split_syrk(c->Dp, ap, s));
     ktimer_end(c, k, s);
@@ -1438,7 +1451,23 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
   }
   ap.prof = dprof ? d_prof : nullptr;
   const size_t k = ktimer_begin(c, pre + ".dspace", s);
-  HIP_TRY(c, launch_solve(c->Dp, ap, s));
+  if (side_split) {
+    SolveArgs af = ap;  // queue positions [0, n_split): the split entities
+    af.n_rows = ap.n_split;
+    HIP_TRY(c, launch_solve(c->Dp, af, aux));
+    HIP_TRY(c, hipEventRecord(c->ev_join, aux));
+    SolveArgs ar = ap;  // positions [n_split, n_rows)
+    ar.order = ap.order + ap.n_split;
+    ar.n_rows = ap.n_rows - ap.n_split;
+    ar.split = nullptr;
+    ar.n_split = 0;
+    ar.work = nullptr;
+    ar.n_work = 0;
+    HIP_TRY(c, launch_solve(c->Dp, ar, s));
+    HIP_TRY(c, hipStreamWaitEvent(s, c->ev_join, 0));
+  } else {
+    HIP_TRY(c, launch_solve(c->Dp, ap, s));
+  }
   ktimer_end(c, k, s);
   {  // the split entities' SYRK is the split kernel's work, their solve this one's
     const double d = c->dim;
@@ -1572,8 +1601,11 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
     const std::string pre = names[side];
     ScopedTimer t(c, names[side]);
     if (!dual || n_dspace >= n_nonempty) {
+      // stream2 (the mixed path's d-space stream) is idle here: the slabs of
+      // the long histories run on it beside the other entities' solve
       rc = launch_dspace(c, a, hs, heff, c->stream, pre,
-                         c->Dp >= 32 && (int64_t)hs.size() == c->order_n[side], side, vkind);
+                         c->Dp >= 32 && (int64_t)hs.size() == c->order_n[side], side, vkind,
+                         c->dual_serial ? nullptr : c->stream2);
       if (rc) return rc;
     } else {
       // d-space solve of the long histories on stream2, concurrently with

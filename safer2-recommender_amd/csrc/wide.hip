@@ -119,6 +119,12 @@ __device__ __forceinline__ bool xcd_unit(int P, int64_t n_units, int64_t& unit, 
 // are loaded one iteration ahead, row ids three ahead.  Two-level
 // accumulation as wide_syrk_kernel (flush into the unit's output tiles
 // every W2FLUSH chunks).
+// 1: the wide Cholesky's tile products (panel sums, diagonal updates) on the
+// bf16 matrix cores with 3-piece split operands (common.h mfma_x6).
+#ifndef FRECSYS_WIDE_CHOL_X6
+#define FRECSYS_WIDE_CHOL_X6 0
+#endif
+
 constexpr int WB2 = 256;
 constexpr int W2R = 16;
 constexpr int W2RING = 4;
@@ -206,6 +212,39 @@ __global__ void __launch_bounds__(512)
           bw = 1.0f;
         }
       }
+    }
+  };
+  // the same split in two stages for the main loop, every load unconditional
+  // (past the end it re-reads the last row; the selects come at use): the
+  // row id of chunk c, then its weight operand (other_weight[id] for the V
+  // kinds, the row weight of a weighted Gramian), then the finished values
+  auto ring_idl = [&](int c) __attribute__((always_inline)) {
+    const int64_t k = kbase + (int64_t)c * W2R + tid;
+    const int64_t kc = k < klim ? k : klim - 1;
+    if (MODE == 0) return (int)(r0 + kc);
+    return a.col[p0 + wide_virt_pos(kc, h)];
+  };
+  auto ring_wraw = [&](int c, int id) __attribute__((always_inline)) {
+    const int64_t k = kbase + (int64_t)c * W2R + tid;
+    const int64_t kc = k < klim ? k : klim - 1;
+    if (MODE == 0) return g.w ? g.w[r0 + kc] : 1.0f;
+    return vk ? a.other_weight[id] : 1.0f;
+  };
+  auto ring_fin = [&](int c, int& id, float w, float& sa, float& bw) __attribute__((always_inline)) {
+    const int64_t k = kbase + (int64_t)c * W2R + tid;
+    if (k >= klim) {
+      id = -1;
+      sa = 0.0f;
+      bw = 0.0f;
+    } else if (MODE == 0) {
+      sa = 1.0f;
+      bw = w;
+    } else if (vk) {
+      sa = sqrtf(w);
+      bw = (k < h && sa > 0.0f) ? w / sa : 0.0f;
+    } else {
+      sa = 1.0f;
+      bw = 1.0f;
     }
   };
   auto ring_store = [&](int c, int id, float sa, float bw) __attribute__((always_inline)) {
@@ -329,6 +368,16 @@ __global__ void __launch_bounds__(512)
     load(0, xr0);
     stage_write(xr0, 0, 0);
   }
+  // ring pipeline of the wave-0 threads: chunk c+4's id is issued at the top
+  // of iteration c, its weight operand at the end of c (after the MFMAs that
+  // cover the id), and the finished values are stored at the end of c+1 --
+  // every load a full iteration of MFMAs old when it is waited on
+  int id4 = -1, id3 = -1;
+  float w3 = 0.0f;
+  if (tid < W2R && nchunks > 3) {
+    id3 = ring_idl(3);
+    w3 = ring_wraw(3, id3);
+  }
   if (nchunks > 1) load(1, xr0);
   lds_barrier();
 
@@ -343,9 +392,7 @@ __global__ void __launch_bounds__(512)
       const int buf = c & 1;
       const bool more = c + 1 < nchunks;
       const bool ring_more = (tid < W2R) && (c + 3 < nchunks);
-      int nid = -1;
-      float nsa = 0.f, nbw = 0.f;
-      if (ring_more) ring_load(c + 3, nid, nsa, nbw);
+      if (tid < W2R && c + 4 < nchunks) id4 = ring_idl(c + 4);
       const bf16x8* st = stage[buf];
       bf16x8* sto = stage[buf ^ 1];
       const int nbase = ((c + 1) % W2RING) * W2R + 8 * hh0;
@@ -393,8 +440,17 @@ __global__ void __launch_bounds__(512)
       // placed after load(c+2) that wait -- in-order counters, a conditional
       // load between -- was vmcnt(0), wave 0 stalling on the rows it had just
       // requested (a full HBM latency per chunk, every wave behind it at the
-      // barrier)
-      if (ring_more) ring_store(c + 3, nid, nsa, nbw);
+      // barrier).  Chunk c+3's values were loaded an iteration ago.
+      if (ring_more) {
+        float sa, bw;
+        int id = id3;
+        ring_fin(c + 3, id, w3, sa, bw);
+        ring_store(c + 3, id, sa, bw);
+      }
+      if (tid < W2R && c + 4 < nchunks) {
+        id3 = id4;
+        w3 = ring_wraw(c + 4, id4);
+      }
       // unconditional (past the end it re-gathers the last chunk, whose ring
       // slot stays valid; never staged): a conditional load here made the
       // waitcnt pass flush vmcnt at the loop head, stalling on these rows
@@ -677,21 +733,47 @@ __global__ void __launch_bounds__(512)
       for (int j = 0; j < 4; ++j) c[4 * g + j] = v[j];
     }
     f32x4v cur[4], nxt[4];
+    // X6: lane half hi takes k = 16 g + 8 hi + j (the bf16 fragment order),
+    // else k = 16 hi + s
+    auto ltile = [&](int q) __attribute__((always_inline)) {
+      return gtile(I, q) + lo * 32 + (FRECSYS_WIDE_CHOL_X6 ? 8 : 16) * hi;
+    };
     if (p > 0) {
-      const f32x4v* L0 = reinterpret_cast<const f32x4v*>(gtile(I, 0) + lo * 32 + 16 * hi);
+      const float* L0 = ltile(0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = L0[j];
+      for (int j = 0; j < 4; ++j)
+        cur[j] = *reinterpret_cast<const f32x4v*>(L0 + (FRECSYS_WIDE_CHOL_X6 ? 16 * (j >> 1) + 4 * (j & 1) : 4 * j));
     }
 #pragma unroll 1
     for (int q = 0; q < p; ++q) {
       if (q + 1 < p) {
-        const f32x4v* Ln = reinterpret_cast<const f32x4v*>(gtile(I, q + 1) + lo * 32 + 16 * hi);
+        const float* Ln = ltile(q + 1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) nxt[j] = Ln[j];
+        for (int j = 0; j < 4; ++j)
+          nxt[j] = *reinterpret_cast<const f32x4v*>(Ln + (FRECSYS_WIDE_CHOL_X6 ? 16 * (j >> 1) + 4 * (j & 1) : 4 * j));
       }
-      const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+      if constexpr (FRECSYS_WIDE_CHOL_X6) {
+        // split-bf16 products (common.h mfma_x6): -L_pq from LDS, L_Iq from
+        // the registers, both split into three bf16 pieces here
+        const float* P = rowL + q * LP + lo * 33 + 8 * hi;
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
+        for (int g = 0; g < 2; ++g) {
+          float pv[8], lv[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            pv[j] = -P[16 * g + j];
+            lv[j] = cur[2 * g + (j >> 2)][j & 3];
+          }
+          bf16x8 pf[3], lf[3];
+          split3x8(pv, pf);
+          split3x8(lv, lf);
+          c = mfma_x6(pf, lf, c);
+        }
+      } else {
+        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
     }
@@ -742,9 +824,26 @@ __global__ void __launch_bounds__(512)
       for (int q = 0; q < 16; ++q) d[q] = App[acc_row(q, hi) * 32 + lo];
 #pragma unroll 1
       for (int q = 0; q < p; ++q) {  // d -= L_pq L_pq^T (k = 16 hi + s)
-        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+        if constexpr (FRECSYS_WIDE_CHOL_X6) {
+          const float* P = rowL + q * LP + lo * 33 + 8 * hi;
 #pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
+          for (int g = 0; g < 2; ++g) {
+            float pv[8], nv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              pv[j] = P[16 * g + j];
+              nv[j] = -pv[j];
+            }
+            bf16x8 pf[3], nf[3];
+            split3x8(pv, pf);
+            split3x8(nv, nf);
+            d = mfma_x6(nf, pf, d);
+          }
+        } else {
+          const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
+        }
       }
       // opaque copies of the lane coordinates: the 48 swizzled / padded
       // addresses below are formed here with a few VALU ops each, not hoisted

@@ -84,3 +84,22 @@ def test_split_deterministic(monkeypatch, quirk_data):
         ctx.solve_side(fh.SIDE_ITEM, fh.KIND_IALS, 0.003, 0.1)
         outs.append(ctx.get_embeddings(fh.SIDE_ITEM))
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("dim", [64, 256])
+def test_split_side_stream_bitwise(monkeypatch, quirk_data, dim):
+    """With every entity in d space, the slabs of the long histories and then
+    their entities' solves run on a second stream beside the other entities'
+    solve; the result is bitwise the single-stream one (FRECSYS_DUAL_SERIAL=1,
+    read when the context is created)."""
+    monkeypatch.setenv("FRECSYS_SPLIT_ROWS", "32")
+    nu, ni, up, uc, ip, ic = quirk_data
+    outs = []
+    for serial in ("1", "0"):
+        monkeypatch.setenv("FRECSYS_DUAL_SERIAL", serial)
+        ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
+        ctx.gramian(fh.SIDE_USER)
+        ctx.solve_side(fh.SIDE_ITEM, fh.KIND_IALS, 0.003, 0.1)
+        assert ctx.timing("solve_item.split")[1] == 1
+        outs.append(ctx.get_embeddings(fh.SIDE_ITEM))
+    np.testing.assert_array_equal(outs[0], outs[1])
