@@ -368,16 +368,18 @@ __global__ void __launch_bounds__(512)
     load(0, xr0);
     stage_write(xr0, 0, 0);
   }
-  // ring pipeline of the wave-0 threads: chunk c+4's id is issued at the top
-  // of iteration c, its weight operand at the end of c (after the MFMAs that
-  // cover the id), and the finished values are stored at the end of c+1 --
-  // every load a full iteration of MFMAs old when it is waited on
-  int id4 = -1, id3 = -1;
-  float w3 = 0.0f;
+  // ring pipeline of the wave-0 threads, issued at the end of each iteration
+  // before the rows it gathers (so that waiting for those rows, in order,
+  // never waits for a ring load younger than them): chunk x's id at the end
+  // of iteration x-5, its weight operand at the end of x-4 (the id an
+  // iteration old), the finished values stored at the end of x-3
+  int idA = -1, idB = -1;  // chunks c+4 (id in flight) and c+3 (id, weight)
+  float wB = 0.0f;
   if (tid < W2R && nchunks > 3) {
-    id3 = ring_idl(3);
-    w3 = ring_wraw(3, id3);
+    idB = ring_idl(3);
+    wB = ring_wraw(3, idB);
   }
+  if (tid < W2R && nchunks > 4) idA = ring_idl(4);
   if (nchunks > 1) load(1, xr0);
   lds_barrier();
 
@@ -392,7 +394,6 @@ __global__ void __launch_bounds__(512)
       const int buf = c & 1;
       const bool more = c + 1 < nchunks;
       const bool ring_more = (tid < W2R) && (c + 3 < nchunks);
-      if (tid < W2R && c + 4 < nchunks) id4 = ring_idl(c + 4);
       const bf16x8* st = stage[buf];
       bf16x8* sto = stage[buf ^ 1];
       const int nbase = ((c + 1) % W2RING) * W2R + 8 * hh0;
@@ -443,14 +444,15 @@ __global__ void __launch_bounds__(512)
       // barrier).  Chunk c+3's values were loaded an iteration ago.
       if (ring_more) {
         float sa, bw;
-        int id = id3;
-        ring_fin(c + 3, id, w3, sa, bw);
+        int id = idB;
+        ring_fin(c + 3, id, wB, sa, bw);
         ring_store(c + 3, id, sa, bw);
       }
       if (tid < W2R && c + 4 < nchunks) {
-        id3 = id4;
-        w3 = ring_wraw(c + 4, id4);
+        idB = idA;
+        wB = ring_wraw(c + 4, idA);
       }
+      if (tid < W2R && c + 5 < nchunks) idA = ring_idl(c + 5);
       // unconditional (past the end it re-gathers the last chunk, whose ring
       // slot stays valid; never staged): a conditional load here made the
       // waitcnt pass flush vmcnt at the loop head, stalling on these rows

@@ -2,6 +2,7 @@ set -o pipefail
 OUT=gpurun_out/r4h
 mkdir -p $OUT
 LIB=safer2-recommender_amd/frecsys_hip/libfrecsys_hip.so
+md5sum $LIB ab/libfrecsys_hip_oldring.so
 cp $LIB $OUT/new.so.bak
 restore() { cp $OUT/new.so.bak $LIB; }
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_wide_split_gpu.py tests/test_wide_gpu.py tests/test_parity_gpu.py tests/test_sharded_gpu.py tests/test_split_gpu.py > $OUT/pytest.log 2>&1; rc=$?
