@@ -223,21 +223,6 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     const int64_t k = k0 + (int64_t)c * R + tid;
     return k < k1 ? a.col[p0 + virt_pos(k, h)] : -1;
   };
-  auto ring_weights = [&](int c, int id, float& sa, float& bw) {
-    const int64_t k = k0 + (int64_t)c * R + tid;
-    sa = 0.0f;
-    bw = 0.0f;
-    if (k < k1) {
-      if (vk) {
-        const float nu = a.other_weight[id];
-        sa = sqrtf(nu);
-        bw = (k < h && sa > 0.0f) ? nu / sa : 0.0f;
-      } else {
-        sa = 1.0f;
-        bw = 1.0f;
-      }
-    }
-  };
   auto ring_store = [&](int c, int id, float sa, float bw) {
     const int s = (c % kRing) * R + tid;
     ring_id[s] = id;
@@ -521,6 +506,13 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     }
     if (nchunks > 1) load_bf(1, xa);
     lds_barrier();
+    // the ring's weights trail its ids by one iteration: chunk c+3's id is
+    // loaded at the top of step c and stored at its end (step c+1's row
+    // gathers read it), its weight operand (other_weight[id], V kinds) is
+    // issued then and its sa / bw stored at the end of step c+1 (step c+2
+    // scales with them) -- so no wait at the end of a step is behind the row
+    // gathers issued at its top (in-order vmcnt)
+    float wpend = 0.0f;  // raw weight of chunk c+2 at the top of step c
     auto step = [&](int c, float (&xcur)[16], float (&xnxt)[16], auto pc)
                     __attribute__((always_inline)) {
       const int buf = c & 1;
@@ -606,10 +598,25 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
         for (int k = 0; k < SLOTS; ++k) split_slot(k);
       }
       if (live) write_bf(buf ^ 1, f);
+      if (tid < R && c >= 1 && c + 2 < nchunks) {  // chunk c+2's sa / bw
+        const int64_t k = k0 + (int64_t)(c + 2) * R + tid;
+        float sa = 0.0f, bw = 0.0f;
+        if (k < k1) {
+          if (vk) {
+            sa = sqrtf(wpend);
+            bw = (k < h && sa > 0.0f) ? wpend / sa : 0.0f;
+          } else {
+            sa = 1.0f;
+            bw = 1.0f;
+          }
+        }
+        const int s = ((c + 2) % kRing) * R + tid;
+        ring_sa[s] = sa;
+        ring_bw[s] = bw;
+      }
       if (ring_more) {
-        float nsa, nbw;
-        ring_weights(c + 3, nid, nsa, nbw);
-        ring_store(c + 3, nid, nsa, nbw);
+        ring_id[((c + 3) % kRing) * R + tid] = nid;
+        if (vk) wpend = a.other_weight[max(nid, 0)];
       }
       lds_barrier();
     };
