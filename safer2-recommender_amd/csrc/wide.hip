@@ -274,11 +274,13 @@ __global__ void __launch_bounds__(512)
         // no select on the loaded value (rows past the end have sa = 0): the
         // loads stay in flight through the MFMAs of the current chunk.  32-bit
         // element offsets while rows x Dp < 2^32 (OFF64 above: gather_off64)
-        float v;
-        if constexpr (OFF64)
-          v = X[(int64_t)max(id[j], 0) * Dp + xcol];
-        else
-          v = X[(unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)xcol];
+        float v = 1.0f;
+        if (!FRECSYS_SKIP(a.debug_skip, 2048)) {  // ablation: no gather at all
+          if constexpr (OFF64)
+            v = X[(int64_t)max(id[j], 0) * Dp + xcol];
+          else
+            v = X[(unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)xcol];
+        }
         xr[4 * q + j] = FRECSYS_SKIP(a.debug_skip, 32) ? 0.0f : v;
       }
     }
@@ -296,7 +298,13 @@ __global__ void __launch_bounds__(512)
     if (bown) bpart += sb.y * x;
     if (wside) x *= sb.y;
     __bf16 ph, pm, pl;
-    split3(x, ph, pm, pl);
+    if (FRECSYS_SKIP(a.debug_skip, 1024)) {  // ablation: one conversion, no split
+      ph = (__bf16)x;
+      pm = ph;
+      pl = ph;
+    } else {
+      split3(x, ph, pm, pl);
+    }
     f[0][j] = ph;
     f[1][j] = pm;
     f[2][j] = pl;
