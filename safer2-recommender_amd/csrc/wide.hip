@@ -119,12 +119,6 @@ __device__ __forceinline__ bool xcd_unit(int P, int64_t n_units, int64_t& unit, 
 // are loaded one iteration ahead, row ids three ahead.  Two-level
 // accumulation as wide_syrk_kernel (flush into the unit's output tiles
 // every W2FLUSH chunks).
-// 1: the wide Cholesky's tile products (panel sums, diagonal updates) on the
-// bf16 matrix cores with 3-piece split operands (common.h mfma_x6).
-#ifndef FRECSYS_WIDE_CHOL_X6
-#define FRECSYS_WIDE_CHOL_X6 0
-#endif
-
 constexpr int WB2 = 256;
 constexpr int W2R = 16;
 constexpr int W2RING = 4;
@@ -743,47 +737,21 @@ __global__ void __launch_bounds__(512)
       for (int j = 0; j < 4; ++j) c[4 * g + j] = v[j];
     }
     f32x4v cur[4], nxt[4];
-    // X6: lane half hi takes k = 16 g + 8 hi + j (the bf16 fragment order),
-    // else k = 16 hi + s
-    auto ltile = [&](int q) __attribute__((always_inline)) {
-      return gtile(I, q) + lo * 32 + (FRECSYS_WIDE_CHOL_X6 ? 8 : 16) * hi;
-    };
     if (p > 0) {
-      const float* L0 = ltile(0);
+      const f32x4v* L0 = reinterpret_cast<const f32x4v*>(gtile(I, 0) + lo * 32 + 16 * hi);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        cur[j] = *reinterpret_cast<const f32x4v*>(L0 + (FRECSYS_WIDE_CHOL_X6 ? 16 * (j >> 1) + 4 * (j & 1) : 4 * j));
+      for (int j = 0; j < 4; ++j) cur[j] = L0[j];
     }
 #pragma unroll 1
     for (int q = 0; q < p; ++q) {
       if (q + 1 < p) {
-        const float* Ln = ltile(q + 1);
+        const f32x4v* Ln = reinterpret_cast<const f32x4v*>(gtile(I, q + 1) + lo * 32 + 16 * hi);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          nxt[j] = *reinterpret_cast<const f32x4v*>(Ln + (FRECSYS_WIDE_CHOL_X6 ? 16 * (j >> 1) + 4 * (j & 1) : 4 * j));
+        for (int j = 0; j < 4; ++j) nxt[j] = Ln[j];
       }
-      if constexpr (FRECSYS_WIDE_CHOL_X6) {
-        // split-bf16 products (common.h mfma_x6): -L_pq from LDS, L_Iq from
-        // the registers, both split into three bf16 pieces here
-        const float* P = rowL + q * LP + lo * 33 + 8 * hi;
+      const float* P = rowL + q * LP + lo * 33 + 16 * hi;
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          float pv[8], lv[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            pv[j] = -P[16 * g + j];
-            lv[j] = cur[2 * g + (j >> 2)][j & 3];
-          }
-          bf16x8 pf[3], lf[3];
-          split3x8(pv, pf);
-          split3x8(lv, lf);
-          c = mfma_x6(pf, lf, c);
-        }
-      } else {
-        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
-      }
+      for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
 #pragma unroll
       for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
     }
@@ -834,26 +802,9 @@ __global__ void __launch_bounds__(512)
       for (int q = 0; q < 16; ++q) d[q] = App[acc_row(q, hi) * 32 + lo];
 #pragma unroll 1
       for (int q = 0; q < p; ++q) {  // d -= L_pq L_pq^T (k = 16 hi + s)
-        if constexpr (FRECSYS_WIDE_CHOL_X6) {
-          const float* P = rowL + q * LP + lo * 33 + 8 * hi;
+        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
 #pragma unroll
-          for (int g = 0; g < 2; ++g) {
-            float pv[8], nv[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              pv[j] = P[16 * g + j];
-              nv[j] = -pv[j];
-            }
-            bf16x8 pf[3], nf[3];
-            split3x8(pv, pf);
-            split3x8(nv, nf);
-            d = mfma_x6(nf, pf, d);
-          }
-        } else {
-          const float* P = rowL + q * LP + lo * 33 + 16 * hi;
-#pragma unroll
-          for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
-        }
+        for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
       }
       // opaque copies of the lane coordinates: the 48 swizzled / padded
       // addresses below are formed here with a few VALU ops each, not hoisted

@@ -25,3 +25,9 @@ for m in 1 1025 2049 3073; do
 done
 restore
 rm -f $OUT/new.so.bak
+for rep in 1 2; do
+  for s in 4096 2048; do
+    FRECSYS_SPLIT_ROWS=$s timeout -k 10 300 python bench.py --allow-env --workload ials_ml20m_d256 --extras= --cpu-seconds 0 --steps 10 --warmup 2 --quiet > $OUT/ml20_split${s}_$rep.json 2> $OUT/ml20_split${s}_$rep.err || { echo bench failed; exit 8; }
+    summ $OUT/ml20_split${s}_$rep.json ml20_split${s}_$rep
+  done
+done
