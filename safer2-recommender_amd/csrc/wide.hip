@@ -268,13 +268,11 @@ __global__ void __launch_bounds__(512)
         // no select on the loaded value (rows past the end have sa = 0): the
         // loads stay in flight through the MFMAs of the current chunk.  32-bit
         // element offsets while rows x Dp < 2^32 (OFF64 above: gather_off64)
-        float v = 1.0f;
-        if (!FRECSYS_SKIP(a.debug_skip, 2048)) {  // ablation: no gather at all
-          if constexpr (OFF64)
-            v = X[(int64_t)max(id[j], 0) * Dp + xcol];
-          else
-            v = X[(unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)xcol];
-        }
+        float v;
+        if constexpr (OFF64)
+          v = X[(int64_t)max(id[j], 0) * Dp + xcol];
+        else
+          v = X[(unsigned)max(id[j], 0) * (unsigned)Dp + (unsigned)xcol];
         xr[4 * q + j] = FRECSYS_SKIP(a.debug_skip, 32) ? 0.0f : v;
       }
     }
