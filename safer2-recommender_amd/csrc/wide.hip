@@ -121,7 +121,13 @@ __device__ __forceinline__ bool xcd_unit(int P, int64_t n_units, int64_t& unit, 
 // every W2FLUSH chunks).
 constexpr int WB2 = 256;
 constexpr int W2R = 16;
-constexpr int W2RING = 4;
+// rows gathered W2AH chunks ahead of their staging (FRECSYS_W2_AH, 1 or 2)
+#ifndef FRECSYS_W2_AH
+#define FRECSYS_W2_AH 1
+#endif
+constexpr int W2AH = FRECSYS_W2_AH;
+static_assert(W2AH == 1 || W2AH == 2, "one or two chunks ahead");
+constexpr int W2RING = W2AH == 1 ? 4 : 8;
 constexpr int W2FLUSH = 128;
 constexpr int W2GRAN = 6 * 512;  // 16-B granules per stage buffer
 
@@ -254,7 +260,7 @@ __global__ void __launch_bounds__(512)
   const bool wside = MODE == 0 && !same && sc >= WB2;  // weighted B operand
   const bool bown = MODE >= 1 && dgp;                  // diagonal pairs form b
   // the staged rows of the next chunk, loaded one iteration before it is staged
-  float xr0[16];
+  float xr0[16], xr1[W2AH == 2 ? 16 : 1];
   auto load = [&](int c, float (&xr)[16]) __attribute__((always_inline)) {
     const int base = (c % W2RING) * W2R + 8 * hh0;
     const int4* ids4 = reinterpret_cast<const int4*>(ring_id + base);  // base % 8 == 0
@@ -355,7 +361,7 @@ __global__ void __launch_bounds__(512)
 
   if (tid < W2R) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < 2 + W2AH; ++c)
       if (c < nchunks) {
         int id;
         float sa, bw;
@@ -373,14 +379,20 @@ __global__ void __launch_bounds__(512)
   // never waits for a ring load younger than them): chunk x's id at the end
   // of iteration x-5, its weight operand at the end of x-4 (the id an
   // iteration old), the finished values stored at the end of x-3
-  int idA = -1, idB = -1;  // chunks c+4 (id in flight) and c+3 (id, weight)
+  // (with W2AH = 2 every distance one chunk longer)
+  int idA = -1, idB = -1;  // chunks c+3+W2AH (id in flight) and c+2+W2AH (id, weight)
   float wB = 0.0f;
-  if (tid < W2R && nchunks > 3) {
-    idB = ring_idl(3);
-    wB = ring_wraw(3, idB);
+  if (tid < W2R && nchunks > 2 + W2AH) {
+    idB = ring_idl(2 + W2AH);
+    wB = ring_wraw(2 + W2AH, idB);
   }
-  if (tid < W2R && nchunks > 4) idA = ring_idl(4);
-  if (nchunks > 1) load(1, xr0);
+  if (tid < W2R && nchunks > 3 + W2AH) idA = ring_idl(3 + W2AH);
+  if constexpr (W2AH == 2) {
+    if (nchunks > 1) load(1, xr1);
+    if (nchunks > 2) load(2, xr0);
+  } else {
+    if (nchunks > 1) load(1, xr0);
+  }
   lds_barrier();
 
   // chunk c: the MFMAs of its tiles, with chunk c+1's staging math (rows
@@ -392,8 +404,9 @@ __global__ void __launch_bounds__(512)
       constexpr bool SAME = decltype(same_c)::value;
       constexpr int NV = SAME ? 8 : 16, PER = NV / MT;
       const int buf = c & 1;
+      const bool live = c < nchunks;  // W2AH = 2: the loop runs an even count
       const bool more = c + 1 < nchunks;
-      const bool ring_more = (tid < W2R) && (c + 3 < nchunks);
+      const bool ring_more = (tid < W2R) && (c + 2 + W2AH < nchunks);
       const bf16x8* st = stage[buf];
       bf16x8* sto = stage[buf ^ 1];
       const int nbase = ((c + 1) % W2RING) * W2R + 8 * hh0;
@@ -405,7 +418,8 @@ __global__ void __launch_bounds__(512)
       }
       // A fragments of the wave's tile row, shared by its tiles; B fragments
       // one tile ahead of their MFMAs
-      bf16x8 af[3], bcur[3], bnxt[3], fs[3];
+      bf16x8 af[3], bcur[3], fs[3];
+      [[maybe_unused]] bf16x8 bnxt[W2AH == 2 ? 1 : 3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
         af[p] = st[g2(p, hi, 32 * tI + lo)];
@@ -413,14 +427,24 @@ __global__ void __launch_bounds__(512)
       }
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        if (tv(m)) {
-          if (m + 1 < MT) {
+        if (tv(m) && live) {
+          if constexpr (W2AH == 2) {
+            // no second fragment set (the registers hold the second chunk
+            // of rows): tile m+1's B fragments read after tile m's MFMAs
+            if (!FRECSYS_SKIP(a.debug_skip, 1)) acc[m] = mfma_x6(af, bcur, acc[m]);
+            if (m + 1 < MT) {
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bnxt[p] = st[g2(p, hi, boff + 32 * (m + 1) + lo)];
+              for (int p = 0; p < 3; ++p) bcur[p] = st[g2(p, hi, boff + 32 * (m + 1) + lo)];
+            }
+          } else {
+            if (m + 1 < MT) {
+#pragma unroll
+              for (int p = 0; p < 3; ++p) bnxt[p] = st[g2(p, hi, boff + 32 * (m + 1) + lo)];
+            }
+            if (!FRECSYS_SKIP(a.debug_skip, 1)) acc[m] = mfma_x6(af, bcur, acc[m]);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bcur[p] = bnxt[p];
           }
-          if (!FRECSYS_SKIP(a.debug_skip, 1)) acc[m] = mfma_x6(af, bcur, acc[m]);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) bcur[p] = bnxt[p];
         }
         if (more) {  // block-uniform
 #pragma unroll
@@ -445,22 +469,32 @@ __global__ void __launch_bounds__(512)
       if (ring_more) {
         float sa, bw;
         int id = idB;
-        ring_fin(c + 3, id, wB, sa, bw);
-        ring_store(c + 3, id, sa, bw);
+        ring_fin(c + 2 + W2AH, id, wB, sa, bw);
+        ring_store(c + 2 + W2AH, id, sa, bw);
       }
-      if (tid < W2R && c + 4 < nchunks) {
+      if (tid < W2R && c + 3 + W2AH < nchunks) {
         idB = idA;
-        wB = ring_wraw(c + 4, idA);
+        wB = ring_wraw(c + 3 + W2AH, idA);
       }
-      if (tid < W2R && c + 5 < nchunks) idA = ring_idl(c + 5);
+      if (tid < W2R && c + 4 + W2AH < nchunks) idA = ring_idl(c + 4 + W2AH);
       // unconditional (past the end it re-gathers the last chunk, whose ring
       // slot stays valid; never staged): a conditional load here made the
       // waitcnt pass flush vmcnt at the loop head, stalling on these rows
-      load(c + 2 < nchunks ? c + 2 : nchunks - 1, xr);
+      load(c + 1 + W2AH < nchunks ? c + 1 + W2AH : nchunks - 1, xr);
       lds_barrier();
   };
   auto run = [&](auto same_c) __attribute__((always_inline)) {
-    for (int c = 0; c < nchunks; ++c) body(same_c, c, xr0);
+    if constexpr (W2AH == 2) {
+      // both register sets in one unconditional body pair (an odd count runs
+      // one idle step): a conditional second step made the compiler wait for
+      // every outstanding row load, one chunk of prefetch in effect
+      for (int c = 0; c < nchunks; c += 2) {
+        body(same_c, c, xr1);
+        body(same_c, c + 1, xr0);
+      }
+    } else {
+      for (int c = 0; c < nchunks; ++c) body(same_c, c, xr0);
+    }
   };
   if (same) run(std::true_type{});
   else run(std::false_type{});
