@@ -123,7 +123,7 @@ constexpr int WB2 = 256;
 constexpr int W2R = 16;
 // rows gathered W2AH chunks ahead of their staging (FRECSYS_W2_AH, 1 or 2)
 #ifndef FRECSYS_W2_AH
-#define FRECSYS_W2_AH 1
+#define FRECSYS_W2_AH 2
 #endif
 constexpr int W2AH = FRECSYS_W2_AH;
 static_assert(W2AH == 1 || W2AH == 2, "one or two chunks ahead");
