@@ -1413,9 +1413,30 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
                       (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (sf * sizeof(float))), s);
       if (rc) return rc;
     }
+    static const bool wprof = getenv("FRECSYS_DUAL_PROF") != nullptr;
+    static unsigned long long* w_prof = nullptr;
+    if (wprof && !w_prof) {
+      HIP_TRY(c, hipMalloc((void**)&w_prof, sizeof(unsigned long long) * 16));
+      HIP_TRY(c, hipMemset(w_prof, 0, sizeof(unsigned long long) * 16));
+    }
+    ap.prof = wprof ? w_prof : nullptr;
     const size_t k = ktimer_begin(c, pre + ".dspace", s);
     HIP_TRY(c, launch_wide_solve(c->Dp, ap, c->wide_ws, batch, s));
     ktimer_end(c, k, s);
+    if (wprof) {  // diagnostics (ablation builds): wide SYRK cycles per chunk and phase
+      unsigned long long hp[16];
+      HIP_TRY(c, hipStreamSynchronize(s));
+      HIP_TRY(c, hipMemcpy(hp, w_prof, sizeof(hp), hipMemcpyDeviceToHost));
+      HIP_TRY(c, hipMemset(w_prof, 0, sizeof(hp)));
+      for (int pt = 0; pt < 2; ++pt)
+        for (int wv = 0; wv < 2; ++wv) {
+          const unsigned long long* q = hp + 8 * pt + 4 * wv;
+          const double n = (double)std::max<unsigned long long>(q[3], 1);
+          fprintf(stderr, "[wide-prof] %s %s wave %d chunks %llu cycles/chunk: mfma+stage %.0f "
+                  "ring+loads %.0f barrier %.0f\n", pre.c_str(), pt ? "diag" : "offdiag",
+                  wv ? 7 : 0, q[3], q[0] / n, q[1] / n, q[2] / n);
+        }
+    }
     // SURVEY 8(d) per entity: dspace_syrk_flops + dspace_solve_flops, gather_bytes
     // (empty histories untouched); both linear in h, so from the prefix sums
     const double d = c->dim;

@@ -395,6 +395,21 @@ __global__ void __launch_bounds__(512)
   }
   lds_barrier();
 
+#ifdef FRECSYS_ABLATION
+  // diagnostics (FRECSYS_DUAL_PROF, ablation builds): per-chunk phase cycles
+  // of waves 0 and 7 (MFMA + staging loop, ring + row-load issue, barrier)
+  const bool tprof = MODE == 1 && a.prof && lane == 0 && (wave == 0 || wave == 7);
+  unsigned long long tp_t = tprof ? clock64() : 0, tp_acc[3] = {0, 0, 0};
+  auto tp_mark = [&](int i) __attribute__((always_inline)) {
+    if (tprof) {
+      const unsigned long long t = clock64();
+      tp_acc[i] += t - tp_t;
+      tp_t = t;
+    }
+  };
+#else
+  auto tp_mark = [](int) {};
+#endif
   // chunk c: the MFMAs of its tiles, with chunk c+1's staging math (rows
   // loaded one iteration ago) spread over the gaps between them -- a slice
   // of NV/8 values after each tile, a granule group stored once complete --
@@ -461,6 +476,7 @@ __global__ void __launch_bounds__(512)
         __builtin_amdgcn_sched_barrier(0);
       }
       if ((c + 1) % W2FLUSH == 0 && more) flush();  // block-uniform
+      tp_mark(0);
       // the ring slot first: its store waits (vmcnt) for the ring loads, and
       // placed after load(c+2) that wait -- in-order counters, a conditional
       // load between -- was vmcnt(0), wave 0 stalling on the rows it had just
@@ -481,7 +497,9 @@ __global__ void __launch_bounds__(512)
       // slot stays valid; never staged): a conditional load here made the
       // waitcnt pass flush vmcnt at the loop head, stalling on these rows
       load(c + 1 + W2AH < nchunks ? c + 1 + W2AH : nchunks - 1, xr);
+      tp_mark(1);
       lds_barrier();
+      tp_mark(2);
   };
   auto run = [&](auto same_c) __attribute__((always_inline)) {
     if constexpr (W2AH == 2) {
@@ -498,6 +516,15 @@ __global__ void __launch_bounds__(512)
   };
   if (same) run(std::true_type{});
   else run(std::false_type{});
+#ifdef FRECSYS_ABLATION
+  if (tprof) {
+    const int o = (wave == 7 ? 4 : 0) + (dgp ? 8 : 0);
+    atomicAdd(a.prof + o + 0, tp_acc[0]);
+    atomicAdd(a.prof + o + 1, tp_acc[1]);
+    atomicAdd(a.prof + o + 2, tp_acc[2]);
+    atomicAdd(a.prof + o + 3, (unsigned long long)nchunks);
+  }
+#endif
   if (flushed) {
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
