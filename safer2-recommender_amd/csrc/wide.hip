@@ -463,7 +463,8 @@ __global__ void __launch_bounds__(512)
   // iteration c: xr holds chunk c+1 (staged now), and then takes chunk c+2
   auto body = [&](auto same_c, int c, float (&xr)[16]) __attribute__((always_inline)) {
       constexpr bool SAME = decltype(same_c)::value;
-      constexpr int NV = SAME ? 8 : 16, PER = NV / MT;
+      // staging slices after the first 8 tile slots (a ninth slot, cmb, has none)
+      constexpr int NV = SAME ? 8 : 16, PER = NV / 8;
       const int buf = c & 1;
       const bool live = c < nchunks;  // W2AH = 2: the loop runs an even count
       const bool more = c + 1 < nchunks;
@@ -515,7 +516,7 @@ __global__ void __launch_bounds__(512)
             for (int p = 0; p < 3; ++p) bcur[p] = bnxt[p];
           }
         }
-        if (more) {  // block-uniform
+        if (more && m < 8) {  // block-uniform
 #pragma unroll
           for (int u = 0; u < PER; ++u) {
             const int r = m * PER + u;
