@@ -133,25 +133,15 @@ constexpr int W2GRAN = 6 * 512;  // 16-B granules per stage buffer
 
 __device__ __forceinline__ int g2(int p, int hh, int c) { return (p * 2 + hh) * 512 + c; }
 
-// Block pairs of one unit: every (I, J), I >= J, or (cmb) the off-diagonal
-// pairs plus one workgroup per two diagonal blocks (2c+1, 2c): they stage the
-// same columns as the off-diagonal pair (2c+1, 2c), and 2 x 36 tiles make
-// 9 per wave -- 1/3 fewer chunk-steps per entity at Dp = 512.
-__host__ __device__ inline int wide_pairs2(int Dp, bool cmb) {
-  const int nb = Dp / 256;
-  return cmb ? nb * (nb - 1) / 2 + nb / 2 : nb * (nb + 1) / 2;
+int wide_pairs2(int Dp) {
+  const int nb = Dp / WB2;
+  return nb * (nb + 1) / 2;
 }
-// FRECSYS_W2_COMBINE (compile time): 1 = the combined diagonal workgroups
-// (nine accumulator tiles per wave), 0 = one workgroup per block pair
-#ifndef FRECSYS_W2_COMBINE
-#define FRECSYS_W2_COMBINE 0
-#endif
-bool wide_combine() { return FRECSYS_W2_COMBINE != 0; }
 
 template <int MODE, bool OFF64 = false>
 __global__ void __launch_bounds__(512)
     wide_syrk2_kernel(SolveArgs a, GramArgs g, int Dp, int64_t rpb, int64_t pos0, float* ws,
-                      int64_t n_units, int combo) {
+                      int64_t n_units) {
   __shared__ __attribute__((aligned(16))) bf16x8 stage[2][W2GRAN];
   __shared__ __attribute__((aligned(16))) int ring_id[W2RING * W2R];
   __shared__ float2 ring_sb[W2RING * W2R];  // (row scale, rhs / B-side weight)
@@ -161,24 +151,9 @@ __global__ void __launch_bounds__(512)
   const int T = Dp >> 5, NT = T * (T + 1) / 2, NB = Dp / WB2;
   int64_t unit;
   int pidx;
-  if (!xcd_unit(wide_pairs2(Dp, combo != 0), n_units, unit, pidx)) return;
+  if (!xcd_unit(NB * (NB + 1) / 2, n_units, unit, pidx)) return;
   int BI, BJ;
-  // cmb: this workgroup takes the diagonal blocks BI = 2c+1 and BJ = 2c
-  bool cmb = false;
-  if (FRECSYS_W2_COMBINE && combo) {
-    const int noff = NB * (NB - 1) / 2;
-    if (pidx < noff) {  // off-diagonal pair pidx (I > J)
-      BI = 1;
-      while (BI * (BI + 1) / 2 <= pidx) ++BI;
-      BJ = pidx - BI * (BI - 1) / 2;
-    } else {
-      cmb = true;
-      BJ = 2 * (pidx - noff);
-      BI = BJ + 1;
-    }
-  } else {
-    pair_of(pidx, BI, BJ);
-  }
+  pair_of(pidx, BI, BJ);
   const bool dgp = BI == BJ;
   // a diagonal pair stages one block (A = B) unless its B side is weighted
   const bool same = dgp && !(MODE == 0 && g.w != nullptr);
@@ -283,7 +258,7 @@ __global__ void __launch_bounds__(512)
   const int hh0 = same ? (tid >> 8) : 0;
   const int xcol = sc < WB2 ? WB2 * BI + sc : WB2 * BJ + (sc - WB2);
   const bool wside = MODE == 0 && !same && sc >= WB2;  // weighted B operand
-  const bool bown = MODE >= 1 && (dgp || cmb);         // diagonal blocks form b
+  const bool bown = MODE >= 1 && dgp;                  // diagonal pairs form b
   // the staged rows of the next chunk, loaded one iteration before it is staged
   float xr0[16], xr1[W2AH == 2 ? 16 : 1];
   auto load = [&](int c, float (&xr)[16]) __attribute__((always_inline)) {
@@ -309,9 +284,6 @@ __global__ void __launch_bounds__(512)
     }
   };
   float bpart = 0.0f, btot = 0.0f;
-  // cmb: b of the thread's column as the two row halves a diagonal pair's
-  // threads keep (rows 0..7 and 8..15 of each chunk), summed in that order
-  float bp2[2] = {0.0f, 0.0f}, bt2[2] = {0.0f, 0.0f};
   // staging math of one value (row r of the thread's column): scale, rhs
   // part, 3-piece split into the fragment being assembled
   auto stage_val = [&](const float (&xr)[16], int base, int r, bf16x8 (&f)[3], int j)
@@ -321,10 +293,7 @@ __global__ void __launch_bounds__(512)
 #pragma clang fp contract(off)
     const float2 sb = ring_sb[base + r];
     float x = xr[r] * sb.x;
-    if (bown) {
-      if (cmb) bp2[r >> 3] += sb.y * x;
-      else bpart += sb.y * x;
-    }
+    if (bown) bpart += sb.y * x;
     if (wside) x *= sb.y;
     __bf16 ph, pm, pl;
     if (FRECSYS_SKIP(a.debug_skip, 1024)) {  // ablation: one conversion, no split
@@ -356,33 +325,18 @@ __global__ void __launch_bounds__(512)
   // 8 tile columns J (J <= I on a diagonal pair).  I = w for waves 0..3 and
   // 11 - w for 4..7, so the two waves of a SIMD (w, w + 4) hold rows
   // summing to 7: 9 tiles per SIMD on a diagonal pair, 16 on the others.
-  // cmb: tiles m <= tI are row tI of diagonal block BI, the rest row 7 - tI
-  // of diagonal block BJ (tI + 1 and 8 - tI tiles: 9 per wave)
-  constexpr int MT = FRECSYS_W2_COMBINE ? 9 : 8;
+  constexpr int MT = 8;
   const int tI = wave < 4 ? wave : 11 - wave;
   auto tv = [&](int m) __attribute__((always_inline)) {  // wave-uniform
-    return cmb ? true : (m < 8 && (!dgp || m <= tI));
+    return !dgp || m <= tI;
   };
   const int boff = same ? 0 : WB2;  // B operand columns in the staged image
-  // global tile (I, J) of slot m, and its A / B columns in the staged image
-  auto tile_i = [&](int m) __attribute__((always_inline)) {
-    return cmb && m > tI ? 8 * BJ + 7 - tI : 8 * BI + tI;
-  };
-  auto tile_j = [&](int m) __attribute__((always_inline)) {
-    return cmb ? (m <= tI ? 8 * BI + m : 8 * BJ + m - tI - 1) : 8 * BJ + m;
-  };
-  auto acol = [&](int m) __attribute__((always_inline)) {
-    return cmb && m > tI ? WB2 + 32 * (7 - tI) : 32 * tI;
-  };
-  auto bcol = [&](int m) __attribute__((always_inline)) {
-    return cmb ? (m <= tI ? 32 * m : WB2 + 32 * (m - tI - 1)) : boff + 32 * m;
-  };
 
   float* const otile0 = MODE == 0   ? g.partials + unit * NT * 1024
                         : MODE == 1 ? ws + unit * ((int64_t)NT * 1024 + Dp)
                                     : nullptr;  // MODE 2 never flushes (<= W2FLUSH chunks)
   auto otile = [&](int m) __attribute__((always_inline)) {
-    return otile0 + (int64_t)tidx(tile_i(m), tile_j(m)) * 1024;
+    return otile0 + (int64_t)tidx(8 * BI + tI, 8 * BJ + m) * 1024;
   };
   bool flushed = false;
   f32x16 acc[MT];
@@ -463,8 +417,7 @@ __global__ void __launch_bounds__(512)
   // iteration c: xr holds chunk c+1 (staged now), and then takes chunk c+2
   auto body = [&](auto same_c, int c, float (&xr)[16]) __attribute__((always_inline)) {
       constexpr bool SAME = decltype(same_c)::value;
-      // staging slices after the first 8 tile slots (a ninth slot, cmb, has none)
-      constexpr int NV = SAME ? 8 : 16, PER = NV / 8;
+      constexpr int NV = SAME ? 8 : 16, PER = NV / MT;
       const int buf = c & 1;
       const bool live = c < nchunks;  // W2AH = 2: the loop runs an even count
       const bool more = c + 1 < nchunks;
@@ -477,10 +430,6 @@ __global__ void __launch_bounds__(512)
       if ((c + 1) % W2FLUSH == 0 && more) {  // block-uniform
         btot += bpart;
         bpart = 0.0f;
-        bt2[0] += bp2[0];
-        bt2[1] += bp2[1];
-        bp2[0] = 0.0f;
-        bp2[1] = 0.0f;
       }
       // A fragments of the wave's tile row, shared by its tiles; B fragments
       // one tile ahead of their MFMAs
@@ -488,35 +437,31 @@ __global__ void __launch_bounds__(512)
       [[maybe_unused]] bf16x8 bnxt[W2AH == 2 ? 1 : 3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        af[p] = st[g2(p, hi, acol(0) + lo)];
-        bcur[p] = st[g2(p, hi, bcol(0) + lo)];
+        af[p] = st[g2(p, hi, 32 * tI + lo)];
+        bcur[p] = st[g2(p, hi, boff + lo)];
       }
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         if (tv(m) && live) {
-          if (cmb && m == tI + 1) {  // block BJ's row: its A fragments
-#pragma unroll
-            for (int p = 0; p < 3; ++p) af[p] = st[g2(p, hi, acol(m) + lo)];
-          }
           if constexpr (W2AH == 2) {
             // no second fragment set (the registers hold the second chunk
             // of rows): tile m+1's B fragments read after tile m's MFMAs
             if (!FRECSYS_SKIP(a.debug_skip, 1)) acc[m] = mfma_x6(af, bcur, acc[m]);
-            if (m + 1 < MT && tv(m + 1)) {
+            if (m + 1 < MT) {
 #pragma unroll
-              for (int p = 0; p < 3; ++p) bcur[p] = st[g2(p, hi, bcol(m + 1) + lo)];
+              for (int p = 0; p < 3; ++p) bcur[p] = st[g2(p, hi, boff + 32 * (m + 1) + lo)];
             }
           } else {
-            if (m + 1 < MT && tv(m + 1)) {
+            if (m + 1 < MT) {
 #pragma unroll
-              for (int p = 0; p < 3; ++p) bnxt[p] = st[g2(p, hi, bcol(m + 1) + lo)];
+              for (int p = 0; p < 3; ++p) bnxt[p] = st[g2(p, hi, boff + 32 * (m + 1) + lo)];
             }
             if (!FRECSYS_SKIP(a.debug_skip, 1)) acc[m] = mfma_x6(af, bcur, acc[m]);
 #pragma unroll
             for (int p = 0; p < 3; ++p) bcur[p] = bnxt[p];
           }
         }
-        if (more && m < 8) {  // block-uniform
+        if (more) {  // block-uniform
 #pragma unroll
           for (int u = 0; u < PER; ++u) {
             const int r = m * PER + u;
@@ -573,7 +518,7 @@ __global__ void __launch_bounds__(512)
   else run(std::false_type{});
 #ifdef FRECSYS_ABLATION
   if (tprof) {
-    const int o = (wave == 7 ? 4 : 0) + (dgp || cmb ? 8 : 0);
+    const int o = (wave == 7 ? 4 : 0) + (dgp ? 8 : 0);
     atomicAdd(a.prof + o + 0, tp_acc[0]);
     atomicAdd(a.prof + o + 1, tp_acc[1]);
     atomicAdd(a.prof + o + 2, tp_acc[2]);
@@ -595,7 +540,7 @@ __global__ void __launch_bounds__(512)
   // (coalesced); b partials of the diagonal pairs' threads after the tiles
   const size_t slab_floats = (size_t)NT * 1024 + 2 * (size_t)Dp;
   auto stile = [&](const float* sb, int m) __attribute__((always_inline)) {
-    return sb + (int64_t)tidx(tile_i(m), tile_j(m)) * 1024 + lane;
+    return sb + (int64_t)tidx(8 * BI + tI, 8 * BJ + m) * 1024 + lane;
   };
   if (MODE == 2) {
     float* sb = a.slabs + (size_t)a.work[unit].slab * slab_floats;
@@ -608,15 +553,7 @@ __global__ void __launch_bounds__(512)
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // b partials in the diagonal pairs' layout: block B, half hh, column c
-    // at WB2 * 2 * B + WB2 * hh + c
-    if (bown && cmb) {
-      const int blk = sc < WB2 ? BI : BJ, col = sc & (WB2 - 1);
-      sb[(size_t)NT * 1024 + WB2 * 2 * blk + col] = bp2[0];
-      sb[(size_t)NT * 1024 + WB2 * 2 * blk + WB2 + col] = bp2[1];
-    } else if (bown) {
-      sb[(size_t)NT * 1024 + WB2 * 2 * BI + tid] = bpart;
-    }
+    if (bown) sb[(size_t)NT * 1024 + WB2 * 2 * BI + tid] = bpart;
     return;
   }
   if (MODE == 1 && fin) {
@@ -644,15 +581,7 @@ __global__ void __launch_bounds__(512)
         if (tv(m)) acc[m] = j == 0 ? v : acc[m] + v;
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (bown && cmb) {
-        const int blk = sc < WB2 ? BI : BJ, col = sc & (WB2 - 1);
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const float bv = sb[(size_t)NT * 1024 + WB2 * 2 * blk + WB2 * hh + col];
-          if (j + 1 < sp.y) bt2[hh] += bv;
-          else bp2[hh] = bv;
-        }
-      } else if (bown) {
+      if (bown) {
         const float bv = sb[(size_t)NT * 1024 + WB2 * 2 * BI + tid];
         if (j + 1 < sp.y) btot += bv;
         else bpart = bv;
@@ -660,8 +589,6 @@ __global__ void __launch_bounds__(512)
     }
   }
   bpart += btot;
-  bp2[0] += bt2[0];
-  bp2[1] += bt2[1];
 
   if (MODE == 0) {
 #pragma unroll
@@ -693,7 +620,7 @@ __global__ void __launch_bounds__(512)
     float gnx[16];
     auto ldg = [&](int m) __attribute__((always_inline)) {
       if (tv(m)) {
-        const int I = tile_i(m), J = tile_j(m);
+        const int I = 8 * BI + tI, J = 8 * BJ + m;
 #pragma unroll
         for (int q = 0; q < 16; ++q)
           gnx[q] = a.G[(int64_t)(32 * I + acc_row(q, hi)) * Dp + 32 * J + lo];
@@ -708,7 +635,7 @@ __global__ void __launch_bounds__(512)
       if (m + 1 < MT) ldg(m + 1);
       if (tv(m)) {
         float* t = otile(m);
-        const int I = tile_i(m), J = tile_j(m);
+        const int I = 8 * BI + tI, J = 8 * BJ + m;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int i = acc_row(q, hi);
@@ -735,12 +662,7 @@ __global__ void __launch_bounds__(512)
   else if (is_u_kind(kind)) finish(std::integral_constant<int, 1>{});
   else if (vk) finish(std::integral_constant<int, 2>{});
   else finish(std::integral_constant<int, 0>{});
-  if (bown && cmb) {  // b of both diagonal blocks: each thread's column
-    float b = bp2[0] + bp2[1];
-    if (is_u_kind(kind)) b *= us;
-    const int blk = sc < WB2 ? BI : BJ, col = sc & (WB2 - 1);
-    ws[unit * ((int64_t)NT * 1024 + Dp) + (int64_t)NT * 1024 + WB2 * blk + col] = b;
-  } else if (bown) {  // b of this diagonal block: the two row halves of each column
+  if (bown) {  // b of this diagonal block: the two row halves of each column
     if (tid >= WB2) bred[sc] = bpart;
     lds_barrier();
     if (tid < WB2) {
@@ -1583,16 +1505,12 @@ hipError_t launch_wide_gram_leaves(int Dp, const GramArgs& g, hipStream_t s) {
   const int64_t nblk = (g.n + g.plan.rpl - 1) / g.plan.rpl;
   if (nblk <= 0) return hipSuccess;
   SolveArgs a{};
-  // a weighted Gramian's diagonal pairs stage both operands: no combining
-  const bool cmb0 = wide_combine() && g.w == nullptr;
   if (gather_off64(g.row0 + g.n, Dp))
-    hipLaunchKernelGGL((wide_syrk2_kernel<0, true>), dim3(xcd_grid(nblk, wide_pairs2(Dp, cmb0))),
-                       dim3(512), 0, s, a, g, Dp, g.plan.rpl, (int64_t)0, (float*)nullptr, nblk,
-                       (int)cmb0);
+    hipLaunchKernelGGL((wide_syrk2_kernel<0, true>), dim3(xcd_grid(nblk, wide_pairs2(Dp))),
+                       dim3(512), 0, s, a, g, Dp, g.plan.rpl, (int64_t)0, (float*)nullptr, nblk);
   else
-    hipLaunchKernelGGL((wide_syrk2_kernel<0, false>), dim3(xcd_grid(nblk, wide_pairs2(Dp, cmb0))),
-                       dim3(512), 0, s, a, g, Dp, g.plan.rpl, (int64_t)0, (float*)nullptr, nblk,
-                       (int)cmb0);
+    hipLaunchKernelGGL((wide_syrk2_kernel<0, false>), dim3(xcd_grid(nblk, wide_pairs2(Dp))),
+                       dim3(512), 0, s, a, g, Dp, g.plan.rpl, (int64_t)0, (float*)nullptr, nblk);
   return hipGetLastError();
 }
 
@@ -1621,26 +1539,25 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
     attr = true;
   }
   const bool grad = is_grad_kind(a.kind);
-  const bool cmb = wide_combine();
   GramArgs g{};
   // the slabs of the long histories (all in the first batch) first
   if (a.n_work > 0) {
     if (a.n_split > std::min<int64_t>(batch, a.n_rows)) return hipErrorInvalidValue;
     if (off64)
-      hipLaunchKernelGGL((wide_syrk2_kernel<2, true>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp, cmb))),
-                         dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work, (int)cmb);
+      hipLaunchKernelGGL((wide_syrk2_kernel<2, true>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
     else
-      hipLaunchKernelGGL((wide_syrk2_kernel<2, false>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp, cmb))),
-                         dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work, (int)cmb);
+      hipLaunchKernelGGL((wide_syrk2_kernel<2, false>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, (int64_t)0, ws, a.n_work);
   }
   for (int64_t s0 = 0; s0 < a.n_rows; s0 += batch) {
     const int64_t nb = std::min<int64_t>(batch, a.n_rows - s0);
     if (off64)
-      hipLaunchKernelGGL((wide_syrk2_kernel<1, true>), dim3(xcd_grid(nb, wide_pairs2(Dp, cmb))),
-                         dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb, (int)cmb);
+      hipLaunchKernelGGL((wide_syrk2_kernel<1, true>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     else
-      hipLaunchKernelGGL((wide_syrk2_kernel<1, false>), dim3(xcd_grid(nb, wide_pairs2(Dp, cmb))),
-                         dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb, (int)cmb);
+      hipLaunchKernelGGL((wide_syrk2_kernel<1, false>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
+                         dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
     else if (Dp == 512)
