@@ -23,13 +23,6 @@
 // With 8 waves: the wave that runs the forward substitution (Y, B of the
 // chain's next block).  Waves w and w + 4 share a SIMD, so 4 leaves the
 // chain wave's SIMD without a worker's tile products beside it.
-// 1: a trailing update U(I, J, p) starts its MFMA accumulator from A_IJ
-// (negated L_Ip operand) and overwrites the tile -- no read-modify-write
-// after the products -- and a worker checks a task's three dependency
-// counters with one LDS wait.
-#ifndef FRECSYS_CHOL_ACC
-#define FRECSYS_CHOL_ACC 0
-#endif
 #ifndef FRECSYS_CHOL_YWAVE
 #define FRECSYS_CHOL_YWAVE 4
 #endif
@@ -245,16 +238,11 @@ __device__ __forceinline__ bool diag_factor_inv(float* tile, int lane) {
   return diag_factor_inv_lds((lds_float*)tile, lane);
 }
 
-// One 32x32 MFMA product u = P Q^T of two LDS tiles (P, Q swizzled);
-// NEG: u = c - P Q^T.
-template <bool NEG = false>
-__device__ __forceinline__ f32x16 tile_pqT(const float* P, const float* Q, int lo, int hi,
-                                           f32x16 u = f32x16{0.f}) {
+// One 32x32 MFMA product u = P Q^T of two LDS tiles (P, Q swizzled).
+__device__ __forceinline__ f32x16 tile_pqT(const float* P, const float* Q, int lo, int hi) {
+  f32x16 u = f32x16{0.f};
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const float pv = P[sw(lo, 2 * s + hi)];
-    u = mfma32(NEG ? -pv : pv, Q[sw(lo, 2 * s + hi)], u);
-  }
+  for (int s = 0; s < 16; ++s) u = mfma32(P[sw(lo, 2 * s + hi)], Q[sw(lo, 2 * s + hi)], u);
   return u;
 }
 
@@ -262,11 +250,10 @@ __device__ __forceinline__ f32x16 tile_pqT(const float* P, const float* Q, int l
 // lane (lo, hi) takes k = 16 g + 8 hi + j of row lo of P and of Q, splits
 // them into three bf16 pieces in registers, and 2 x 6 v_mfma_f32_32x32x16_bf16
 // (32 cycles each) replace 16 v_mfma_f32_32x32x2_f32 (64 cycles each).
-// SAME: P == Q (one operand split, used on both sides).  NEG: u = c - P Q^T
-// (the pieces of -x are exactly the negated pieces of x).
-template <bool SAME = false, bool NEG = false>
-__device__ __forceinline__ f32x16 tile_pqT_x6(const float* P, const float* Q, int lo, int hi,
-                                              f32x16 u = f32x16{0.f}) {
+// SAME: P == Q (one operand split, used on both sides).
+template <bool SAME = false>
+__device__ __forceinline__ f32x16 tile_pqT_x6(const float* P, const float* Q, int lo, int hi) {
+  f32x16 u = f32x16{0.f};
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     float pv[8], qv[8];
@@ -276,24 +263,10 @@ __device__ __forceinline__ f32x16 tile_pqT_x6(const float* P, const float* Q, in
       if (!SAME) qv[j] = Q[sw(lo, 16 * g + 8 * hi + j)];
     }
     bf16x8 pf[3], qf[3];
+    split3x8(pv, pf);
     if (SAME) {
-      split3x8(pv, pf);
-      if constexpr (NEG) {
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-          qf[p] = __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, pf[p]) ^ 0x80008000u);
-        }
-        u = mfma_x6(qf, pf, u);
-      } else {
-        u = mfma_x6(pf, pf, u);
-      }
+      u = mfma_x6(pf, pf, u);
     } else {
-      if constexpr (NEG) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pv[j] = -pv[j];
-      }
-      split3x8(pv, pf);
       split3x8(qv, qf);
       u = mfma_x6(pf, qf, u);
     }
@@ -519,22 +492,11 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
     if (!FRECSYS_SKIP(debug_skip, 8)) {
       const float* Li = tiles + tidx(I, p) * 1024;
       const float* Lj = tiles + tidx(J, p) * 1024;
-      if constexpr (FRECSYS_CHOL_ACC) {
-        f32x16 c;
+      const f32x16 u = !X6     ? tile_pqT(Li, Lj, lo, hi)
+                       : I == J ? tile_pqT_x6<true>(Li, Li, lo, hi)
+                                : tile_pqT_x6(Li, Lj, lo, hi);
 #pragma unroll
-        for (int q = 0; q < 16; ++q) c[q] = Aij[sw(acc_row(q, hi), lo)];
-        const f32x16 u = !X6     ? tile_pqT<true>(Li, Lj, lo, hi, c)
-                         : I == J ? tile_pqT_x6<true, true>(Li, Li, lo, hi, c)
-                                  : tile_pqT_x6<false, true>(Li, Lj, lo, hi, c);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) Aij[sw(acc_row(q, hi), lo)] = u[q];
-      } else {
-        const f32x16 u = !X6     ? tile_pqT(Li, Lj, lo, hi)
-                         : I == J ? tile_pqT_x6<true>(Li, Li, lo, hi)
-                                  : tile_pqT_x6(Li, Lj, lo, hi);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) Aij[sw(acc_row(q, hi), lo)] -= u[q];
-      }
+      for (int q = 0; q < 16; ++q) Aij[sw(acc_row(q, hi), lo)] -= u[q];
     }
     set_ver(ver + tidx(I, J), p + 1, lane);
   };
@@ -621,21 +583,6 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
         wait_ver(f, v);
       }
     };
-    // three counters, one LDS round trip when all are already satisfied
-    auto wwait3 = [&](const int* f1, int v1, const int* f2, int v2, const int* f3, int v3) {
-      const unsigned long long t = prof ? clock64() : 0;
-      const int a1 = *(volatile lds_int*)(f1);
-      const int a2 = *(volatile lds_int*)(f2);
-      const int a3 = *(volatile lds_int*)(f3);
-      if (__builtin_amdgcn_readfirstlane(a1) < v1 || __builtin_amdgcn_readfirstlane(a2) < v2 ||
-          __builtin_amdgcn_readfirstlane(a3) < v3) {
-        wait_ver(f1, v1);
-        wait_ver(f2, v2);
-        wait_ver(f3, v3);
-      }
-      asm volatile("" ::: "memory");
-      if (prof) tww += clock64() - t;
-    };
 #pragma unroll 1
     for (int p = 0; p + 1 < T; ++p) {
 #pragma unroll 1
@@ -652,13 +599,9 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
 #pragma unroll 1
         for (int I = (J == p + 1 ? p + 2 : J); I < T; ++I, ++k) {
           if (wk_wave(k % NWK) != wave) continue;
-          if constexpr (FRECSYS_CHOL_ACC) {
-            wwait3(ver + tidx(I, p), p + 1, ver + tidx(J, p), p + 1, ver + tidx(I, J), p);
-          } else {
-            wwait(ver + tidx(I, p), p + 1);
-            wwait(ver + tidx(J, p), p + 1);
-            wwait(ver + tidx(I, J), p);
-          }
+          wwait(ver + tidx(I, p), p + 1);
+          wwait(ver + tidx(J, p), p + 1);
+          wwait(ver + tidx(I, J), p);
           update(I, J, p);
         }
       }
