@@ -23,6 +23,13 @@
 // With 8 waves: the wave that runs the forward substitution (Y, B of the
 // chain's next block).  Waves w and w + 4 share a SIMD, so 4 leaves the
 // chain wave's SIMD without a worker's tile products beside it.
+// n > 0: a worker raises its issue priority (1; the chain runs at 2) over
+// the worker that shares its SIMD for the panel-p tasks of block rows
+// I <= p + 1 + n -- n = 1: the ones that feed the chain's next block
+// (S(p+2, p), U(p+2, p+1, p), U(p+2, p+2, p)).
+#ifndef FRECSYS_CHOL_WPRIO
+#define FRECSYS_CHOL_WPRIO 1
+#endif
 #ifndef FRECSYS_CHOL_YWAVE
 #define FRECSYS_CHOL_YWAVE 4
 #endif
@@ -583,6 +590,10 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
         wait_ver(f, v);
       }
     };
+    auto wprio = [&](bool c) {
+      if (c) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    };
 #pragma unroll 1
     for (int p = 0; p + 1 < T; ++p) {
 #pragma unroll 1
@@ -590,6 +601,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
         if (wk_wave(k % NWK) != wave) continue;
         wwait(ver + tidx(p, p), p + 1);
         wwait(ver + tidx(I, p), p);
+        if (FRECSYS_CHOL_WPRIO) wprio(I <= p + 1 + FRECSYS_CHOL_WPRIO);
         trsm(I, p);
         wwait(yver, p + 1);
         bupd(I, p);
@@ -602,10 +614,12 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
           wwait(ver + tidx(I, p), p + 1);
           wwait(ver + tidx(J, p), p + 1);
           wwait(ver + tidx(I, J), p);
+          if (FRECSYS_CHOL_WPRIO) wprio(I <= p + 1 + FRECSYS_CHOL_WPRIO);
           update(I, J, p);
         }
       }
     }
+    if (FRECSYS_CHOL_WPRIO) __builtin_amdgcn_s_setprio(0);
     if (prof && lane == 0) {
       atomicAdd(prof + 6, (clock64() - t0) / NWK);
       atomicAdd(prof + 15, tww / NWK);
