@@ -30,6 +30,14 @@
 #ifndef FRECSYS_CHOL_WPRIO
 #define FRECSYS_CHOL_WPRIO 1
 #endif
+// 1: the chain's update of the next diagonal tile, U(p+1, p+1, p), stays
+// in registers and goes straight into its factor F(p+1) (the accumulator
+// layout turned into rows by v_permlane32_swap: the tile is symmetric), so
+// no LDS write + read-back of the tile sits on the chain.  Kernels with the
+// blocked factor and split-bf16 products only.
+#ifndef FRECSYS_CHOL_FUSE
+#define FRECSYS_CHOL_FUSE 1
+#endif
 #ifndef FRECSYS_CHOL_YWAVE
 #define FRECSYS_CHOL_YWAVE 4
 #endif
@@ -146,13 +154,14 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
 // in registers by then), and columns 16..31 by the recurrence over
 // m in [16, k) only.  256 v_readlane + 256 FMAs of the serial chain become
 // MFMAs.
+// The factor from rows already in registers (a: lanes 0..31 row r of A,
+// lanes 32..63 column r of the identity); L^-1 goes to the tile.
 template <int LDP = 0>
-__device__ __forceinline__ bool diag_factor_inv_blk_inl(lds_float* tile, int lane) {
+__device__ __forceinline__ bool diag_factor_inv_blk_regs(float (&a)[32], lds_float* tile,
+                                                         int lane) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   const int r = lane & 31;
   const bool fl = lane < 32;
-  float a[32];
-  load_factor_rows<8, LDP>(tile, r, fl, a);
   // pivot test without a vector compare per column: piv > 0 and not NaN
   // <=> its bits as an int lie in (0, 0x7f800000]
   int pmin = 0x7fffffff, pmax = 0;
@@ -228,6 +237,31 @@ __device__ __forceinline__ bool diag_factor_inv_blk_inl(lds_float* tile, int lan
       if (!fl) tile[tix<LDP>(k, j)] = (k >= j) ? a[k] : 0.0f;
   }
   return ok;
+}
+template <int LDP = 0>
+__device__ __forceinline__ bool diag_factor_inv_blk_inl(lds_float* tile, int lane) {
+  float a[32];
+  load_factor_rows<8, LDP>(tile, lane & 31, lane < 32, a);
+  return diag_factor_inv_blk_regs<LDP>(a, tile, lane);
+}
+// The same from the chain's updated diagonal tile in MFMA accumulator layout
+// (c[q] = element (acc_row(q, hi), lo)): the tile is symmetric, so lane lo's
+// row lo is its own 16 values and lane lo+32's (one v_permlane32_swap each).
+// A call, as diag_factor_inv_blk (the accumulator travels in 16 VGPRs).
+__device__ __noinline__ bool diag_factor_inv_acc(f32x16 c, lds_float* tile) {
+  const int lane = __lane_id();
+  const int r = lane & 31;
+  const bool fl = lane < 32;
+  float a[32];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const auto sv = __builtin_amdgcn_permlane32_swap(__float_as_uint(c[q]),
+                                                     __float_as_uint(c[q]), false, false);
+    const int c0 = acc_row(q, 0), c1 = acc_row(q, 1);
+    a[c0] = fl ? c[q] : (c0 == r ? 1.0f : 0.0f);
+    a[c1] = fl ? __uint_as_float(sv[1]) : (c1 == r ? 1.0f : 0.0f);
+  }
+  return diag_factor_inv_blk_regs<0>(a, tile, lane);
 }
 // As a call: callers with few live registers (the tiled kernels); a caller
 // holding its matrix in registers (solve_rr.hip) inlines the body instead,
@@ -466,6 +500,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   constexpr int NT = T * (T + 1) / 2;
   // split-bf16 tile products where the register budget allows (as BLK)
   constexpr bool X6 = FRECSYS_CHOL_X6 && BLK;
+  constexpr bool FUSE = FRECSYS_CHOL_FUSE && X6 && FRECSYS_DIAG_BLK;
   const unsigned long long t0 = prof ? clock64() : 0;
   const int lane = tid & 63, lo = lane & 31, hi = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -542,18 +577,45 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
     };
 #pragma unroll 1
     for (int p = -1; p + 1 < T; ++p) {  // one factor call site
-      if (p >= 0) {
-        wait_ver(ver + tidx(p + 1, p), p);  // all of panel < p's updates
-        lap(tw);
-        trsm(p + 1, p);
-        if (!YW) bupd(p + 1, p);
-        lap(ts);
-        wait_ver(ver + tidx(p + 1, p + 1), p);
-        lap(tw);
-        update(p + 1, p + 1, p);
-        lap(tu);
+      if constexpr (FUSE) {
+        float* Tnn = tiles + tidx(p + 1, p + 1) * 1024;
+        bool ok = true;
+        if (p >= 0) {
+          wait_ver(ver + tidx(p + 1, p), p);  // all of panel < p's updates
+          lap(tw);
+          trsm(p + 1, p);
+          if (!YW) bupd(p + 1, p);
+          lap(ts);
+          wait_ver(ver + tidx(p + 1, p + 1), p);
+          lap(tw);
+          // A_nn - L_np L_np^T, element (acc_row(q, hi), lo); by symmetry
+          // lane lo's row lo is its own 16 values + lane lo+32's
+          const float* Lnp = tiles + tidx(p + 1, p) * 1024;
+          f32x16 u = f32x16{0.f};
+          if (!FRECSYS_SKIP(debug_skip, 8)) u = tile_pqT_x6<true>(Lnp, Lnp, lo, hi);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) u[q] = Tnn[sw(acc_row(q, hi), lo)] - u[q];
+          lap(tu);
+          if (!FRECSYS_SKIP(debug_skip, 2)) ok = diag_factor_inv_acc(u, (lds_float*)Tnn);
+        } else {
+          if (!FRECSYS_SKIP(debug_skip, 2)) ok = diag_factor_inv_blk((lds_float*)Tnn, lane);
+        }
+        if (!ok && lane == 0) flag[0] = 1;
+        set_ver(ver + tidx(p + 1, p + 1), p + 2, lane);
+      } else {
+        if (p >= 0) {
+          wait_ver(ver + tidx(p + 1, p), p);  // all of panel < p's updates
+          lap(tw);
+          trsm(p + 1, p);
+          if (!YW) bupd(p + 1, p);
+          lap(ts);
+          wait_ver(ver + tidx(p + 1, p + 1), p);
+          lap(tw);
+          update(p + 1, p + 1, p);
+          lap(tu);
+        }
+        factor(p + 1);
       }
-      factor(p + 1);
       if (!YW) ysolve(p + 1);
       lap(tf);
     }
