@@ -84,6 +84,23 @@ __device__ __forceinline__ int tix(int r, int c) {
 template <int G, int LDP = 0>
 __device__ __forceinline__ void load_factor_rows(const lds_float* tile, int r, bool fl,
                                                  float (&a)[32]) {
+  if constexpr (FRECSYS_GSW && LDP == 0) {
+    // the row as 8 granule reads (conflict-free, see common.h sw)
+    typedef __attribute__((address_space(3))) const f32x4v lds_f32x4c;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const f32x4v v = *reinterpret_cast<lds_f32x4c*>(tile + r * 32 + (((g ^ (r >> 1)) & 7) << 2));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[4 * g + t] = v[t];
+    }
+    if constexpr (G == 1) {
+#pragma unroll
+      for (int c = 0; c < 32; ++c) asm volatile("" : "+v"(a[c]));
+    }
+#pragma unroll
+    for (int c = 0; c < 32; ++c) a[c] = fl ? a[c] : (c == r ? 1.0f : 0.0f);
+    return;
+  }
   if constexpr (G == 1) {
 #pragma unroll
     for (int c = 0; c < 32; ++c) {
@@ -280,10 +297,21 @@ __device__ __forceinline__ bool diag_factor_inv(float* tile, int lane) {
 }
 
 // One 32x32 MFMA product u = P Q^T of two LDS tiles (P, Q swizzled).
+// Lane (lo, hi) supplies k = 2s + hi of row lo: with the granule swizzle,
+// one b128 read of row lo's columns 4g .. 4g+3 serves s = 2g and 2g + 1.
 __device__ __forceinline__ f32x16 tile_pqT(const float* P, const float* Q, int lo, int hi) {
   f32x16 u = f32x16{0.f};
+#if FRECSYS_GSW
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const f32x4v pv = row_gran(P, lo, g), qv = row_gran(Q, lo, g);
+    u = mfma32(hi ? pv[1] : pv[0], hi ? qv[1] : qv[0], u);
+    u = mfma32(hi ? pv[3] : pv[2], hi ? qv[3] : qv[2], u);
+  }
+#else
 #pragma unroll
   for (int s = 0; s < 16; ++s) u = mfma32(P[sw(lo, 2 * s + hi)], Q[sw(lo, 2 * s + hi)], u);
+#endif
   return u;
 }
 
@@ -298,11 +326,25 @@ __device__ __forceinline__ f32x16 tile_pqT_x6(const float* P, const float* Q, in
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     float pv[8], qv[8];
+#if FRECSYS_GSW
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const f32x4v p4 = row_gran(P, lo, 4 * g + 2 * hi + h2);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) pv[4 * h2 + t] = p4[t];
+      if (!SAME) {
+        const f32x4v q4 = row_gran(Q, lo, 4 * g + 2 * hi + h2);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) qv[4 * h2 + t] = q4[t];
+      }
+    }
+#else
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       pv[j] = P[sw(lo, 16 * g + 8 * hi + j)];
       if (!SAME) qv[j] = Q[sw(lo, 16 * g + 8 * hi + j)];
     }
+#endif
     bf16x8 pf[3], qf[3];
     split3x8(pv, pf);
     if (SAME) {
@@ -482,11 +524,24 @@ __device__ __forceinline__ void set_ver(int* f, int v, int lane) {
 template <bool TR>
 __device__ __forceinline__ float tile_gemv(const float* M, const float* v, int lo, int hi) {
   float s0 = 0.0f, s1 = 0.0f;
+  if constexpr (!TR && FRECSYS_GSW) {
+    // row lo's columns 16 hi .. +15 as four granule reads
 #pragma unroll
-  for (int m = 0; m < 16; m += 2) {
-    const int m0 = 16 * hi + m;
-    s0 += M[TR ? sw(m0, lo) : sw(lo, m0)] * v[m0];
-    s1 += M[TR ? sw(m0 + 1, lo) : sw(lo, m0 + 1)] * v[m0 + 1];
+    for (int g = 0; g < 4; ++g) {
+      const f32x4v x = row_gran(M, lo, 4 * hi + g);
+      const int m0 = 16 * hi + 4 * g;
+      s0 += x[0] * v[m0];
+      s1 += x[1] * v[m0 + 1];
+      s0 += x[2] * v[m0 + 2];
+      s1 += x[3] * v[m0 + 3];
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < 16; m += 2) {
+      const int m0 = 16 * hi + m;
+      s0 += M[TR ? sw(m0, lo) : sw(lo, m0)] * v[m0];
+      s1 += M[TR ? sw(m0 + 1, lo) : sw(lo, m0 + 1)] * v[m0 + 1];
+    }
   }
   const float s = s0 + s1;
   return s + __shfl_xor(s, 32);

@@ -540,8 +540,12 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
     wave_sync();
     // y_p = L_pp^-1 b_p  (lane lo, both halves compute, half 0 keeps it)
     float yp = 0.0f;
-#pragma unroll 8
-    for (int k = 0; k < 32; ++k) yp += Tpp[sw(lo, k)] * bvec[32 * p + k];
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {  // row lo by granules (common.h row_gran), k ascending
+      const f32x4v x4 = row_gran(Tpp, lo, g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) yp += x4[t] * bvec[32 * p + 4 * g + t];
+    }
     y[p] = yp;
     if (hi == 0) xvec[32 * p + lo] = yp;  // y staged for the panel update
     if (p + 1 < T) {
@@ -553,8 +557,12 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
       wave_sync();
       // b_1 -= L_10 y_0 ; A_11 -= L_10 L_10^T
       float t = 0.0f;
-#pragma unroll 8
-      for (int k = 0; k < 32; ++k) t += A10[sw(lo, k)] * xvec[32 * p + k];
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        const f32x4v x4 = row_gran(A10, lo, g);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t += x4[u] * xvec[32 * p + 4 * g + u];
+      }
       const f32x16 w = tile_pqT(A10, A10, lo, hi);
       float* A11 = tiles + tidx(p + 1, p + 1) * 1024;
       wave_sync();

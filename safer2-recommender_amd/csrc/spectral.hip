@@ -696,7 +696,11 @@ __global__ void __launch_bounds__(1024)
         for (int s = 0; s < 16; ++s) pa[s] = src[2 * s];
         const float* Lk = panel + k * 1024;
 #pragma unroll
-        for (int s = 0; s < 16; ++s) acc = mfma32(pa[s], Lk[sw(lo, 2 * s + hi)], acc);
+        for (int g = 0; g < 8; ++g) {  // row lo of L_ik by granules (k = 2s + hi)
+          const f32x4v l4 = row_gran(Lk, lo, g);
+          acc = mfma32(pa[2 * g], hi ? l4[1] : l4[0], acc);
+          acc = mfma32(pa[2 * g + 1], hi ? l4[3] : l4[2], acc);
+        }
       }
       float* st = stg + wave * 1024;
 #pragma unroll
