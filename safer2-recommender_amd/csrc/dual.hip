@@ -201,6 +201,12 @@ __global__ void __launch_bounds__(256) dual_sweep_kernel(DualArgs a) {
   }
 }
 
+// Smallest bucket whose Cholesky runs the blocked diagonal factor and the
+// split-bf16 tile products (chol.h BLK): TH = 3 spills with them.
+#ifndef FRECSYS_DUAL_BLK_TH
+#define FRECSYS_DUAL_BLK_TH 4
+#endif
+
 template <int TH, bool BF>
 __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
     __attribute__((amdgpu_waves_per_eu(DualCfg<TH, BF>::WPE, 8))) dual_solve_kernel(DualArgs a) {
@@ -464,8 +470,10 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   mark(1);
 #if FRECSYS_CHOL_DF
   // the MFMA-blocked diagonal factor where the register budget allows it
-  // (TH >= 6: one workgroup per CU anyway); TH = 3..5 keep their occupancy
-  chol_solve_df<TH, NW, (TH >= 6)>(tiles, bvec, xvec, part, flag, tid, a.debug_skip, a.prof);
+  // (TH >= 4: with the granule tile layout TH = 4, 5 keep their occupancy
+  // without spills; TH = 3 would spill)
+  chol_solve_df<TH, NW, (TH >= FRECSYS_DUAL_BLK_TH)>(tiles, bvec, xvec, part, flag, tid,
+                                                     a.debug_skip, a.prof);
 #else
   chol_solve_tiles<TH, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
 #endif
