@@ -202,9 +202,9 @@ __global__ void __launch_bounds__(256) dual_sweep_kernel(DualArgs a) {
 }
 
 // Smallest bucket whose Cholesky runs the blocked diagonal factor and the
-// split-bf16 tile products (chol.h BLK): TH = 3 spills with them.
+// split-bf16 tile products (chol.h BLK).
 #ifndef FRECSYS_DUAL_BLK_TH
-#define FRECSYS_DUAL_BLK_TH 4
+#define FRECSYS_DUAL_BLK_TH 3
 #endif
 
 template <int TH, bool BF>
@@ -470,8 +470,9 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   mark(1);
 #if FRECSYS_CHOL_DF
   // the MFMA-blocked diagonal factor where the register budget allows it
-  // (TH >= 4: with the granule tile layout TH = 4, 5 keep their occupancy
-  // without spills; TH = 3 would spill)
+  // (every bucket since the granule tile layout: TH = 4, 5 keep their
+  // occupancy without spills; TH = 3 at 128 registers spills 8, measured
+  // faster all the same)
   chol_solve_df<TH, NW, (TH >= FRECSYS_DUAL_BLK_TH)>(tiles, bvec, xvec, part, flag, tid,
                                                      a.debug_skip, a.prof);
 #else
