@@ -535,6 +535,12 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
 // ---------------------------------------------------------------------
 __device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
 
+// 1: the one-wave solve runs the blocked diagonal factor and split-bf16
+// tile products (chol.h) instead of the plain factor and f32 MFMA.
+#ifndef FRECSYS_WAVE_X6
+#define FRECSYS_WAVE_X6 1
+#endif
+
 // chol_solve_tiles for one wave (T <= 2): x = S^-1 b, S's lower tiles in
 // LDS (swizzled), diagonal tiles become L_pp^-1.
 template <int T>
@@ -545,7 +551,8 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
 #pragma unroll
   for (int p = 0; p < T; ++p) {
     float* Tpp = tiles + tidx(p, p) * 1024;
-    if (!FRECSYS_SKIP(debug_skip, 2) && !diag_factor_inv(Tpp, lane) && lane == 0) flag[0] = 1;
+    if (!FRECSYS_SKIP(debug_skip, 2) && !diag_factor_inv<FRECSYS_WAVE_X6>(Tpp, lane) && lane == 0)
+      flag[0] = 1;
     wave_sync();
     // y_p = L_pp^-1 b_p  (lane lo, both halves compute, half 0 keeps it)
     float yp = 0.0f;
@@ -559,7 +566,8 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
     if (hi == 0) xvec[32 * p + lo] = yp;  // y staged for the panel update
     if (p + 1 < T) {
       float* A10 = tiles + tidx(p + 1, p) * 1024;
-      const f32x16 u = tile_pqT(A10, Tpp, lo, hi);  // L_10 = A_10 L_00^-T
+      const f32x16 u = FRECSYS_WAVE_X6 ? tile_pqT_x6(A10, Tpp, lo, hi)
+                                       : tile_pqT(A10, Tpp, lo, hi);  // L_10 = A_10 L_00^-T
       wave_sync();
 #pragma unroll
       for (int q = 0; q < 16; ++q) A10[sw(acc_row(q, hi), lo)] = u[q];
@@ -572,7 +580,8 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
 #pragma unroll
         for (int u = 0; u < 4; ++u) t += x4[u] * xvec[32 * p + 4 * g + u];
       }
-      const f32x16 w = tile_pqT(A10, A10, lo, hi);
+      const f32x16 w = FRECSYS_WAVE_X6 ? tile_pqT_x6<true>(A10, A10, lo, hi)
+                                       : tile_pqT(A10, A10, lo, hi);
       float* A11 = tiles + tidx(p + 1, p + 1) * 1024;
       wave_sync();
       if (hi == 0) bvec[32 * (p + 1) + lo] -= t;
