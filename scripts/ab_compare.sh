@@ -1,4 +1,4 @@
-# usage: bash scripts/_ab.sh <outdir> <variant...>   (A/B of ab/libfrecsys_hip_<v>.so against the tree's library)
+# usage: bash scripts/ab_compare.sh <outdir under gpurun_out> <variant...>  (A/B of ab/libfrecsys_hip_<v>.so, built by `make abvar`, against the tree's library: GPU parity tests on each variant, alternating bench lines, FRECSYS_DUAL_PROF phase cycles)
 set -o pipefail
 OUT=gpurun_out/$1; shift
 VS="$*"
