@@ -18,10 +18,10 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 CXXFLAGS := -O3 -std=c++17 -Wall -I include -I $(PKG)/include -pthread
 
 HIP_SRCS := $(CSRC)/solve.hip $(CSRC)/dual.hip $(CSRC)/spectral.hip $(CSRC)/gramian.hip \
-            $(CSRC)/loss.hip $(CSRC)/wide.hip $(CSRC)/topk.hip $(CSRC)/pp.hip \
+            $(CSRC)/loss.hip $(CSRC)/wide.hip $(CSRC)/wide_syrk.hip $(CSRC)/topk.hip $(CSRC)/pp.hip \
             $(CSRC)/capi.hip
 HIP_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJ)/%.o,$(HIP_SRCS))
-HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h $(CSRC)/chol.h include/frecsys_hip.h
+HDRS     := $(CSRC)/kernels.h $(CSRC)/common.h $(CSRC)/chol.h $(CSRC)/wide.h include/frecsys_hip.h
 
 .PHONY: all lib oracle run_model model_dump model_lib clean ablation
 all: lib oracle run_model model_dump model_lib
@@ -63,11 +63,13 @@ $(MODELDUMP): tests/cpp/model_dump.cc $(FRECSYS_HDRS) include/frecsys_hip.h $(LI
 # (the shipped library refuses the variable); LD_LIBRARY_PATH / a copy over
 # frecsys_hip/libfrecsys_hip.so swaps it in for an ablation run.
 ABL_LIB := ab/libfrecsys_hip_ablation.so
+ABL_OBJS := $(patsubst $(CSRC)/%.hip,ab/obj/%.o,$(HIP_SRCS))
 ablation: $(ABL_LIB)
-$(ABL_LIB): $(HIP_SRCS) $(HDRS)
+ab/obj/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p ab/obj
-	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) -DFRECSYS_ABLATION -c $$f -o ab/obj/$$(basename $$f .hip).o || exit 1; done
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ ab/obj/*.o -lrccl
+	$(HIPCC) $(HIPFLAGS) -DFRECSYS_ABLATION -c $< -o $@
+$(ABL_LIB): $(ABL_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(ABL_OBJS) -lrccl
 
 # A/B build of the library with extra defines, for a timed comparison on the
 # GPU box (a copy over frecsys_hip/libfrecsys_hip.so swaps it in there), e.g.

@@ -53,6 +53,8 @@ struct SolveArgs {
   float* slabs;                // [slabs][split_slab_floats(Dp)]
   const SplitWork* work;       // [n_work] partial SYRK items
   int64_t n_work;
+  // wide dims: the pre-split copy of X (wide.h wide_xsplit_*), or nullptr
+  const char* xsplit;
 };
 
 // Partition-independent Gramian.  The rows of a side are cut
@@ -284,8 +286,10 @@ int64_t wide_rows_per_leaf(int64_t n);
 hipError_t launch_wide_gram_leaves(int Dp, const GramArgs& g, hipStream_t s);
 hipError_t launch_wide_gram_final(int Dp, const float* gslabs, int64_t ngroup, float* G,
                                   hipStream_t s);
+// xsplit: a buffer of wide_xsplit_bytes(Dp, a.n_other) (wide.h) for the SYRK
+// from the pre-split table, or nullptr for the register-staged SYRK
 hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batch,
-                             hipStream_t s);
+                             hipStream_t s, char* xsplit = nullptr);
 size_t wide_tridiag_work_floats(int Dp);
 bool wide_tridiag_tagged();
 hipError_t launch_wide_tridiag(const float* G, int Dp, float* tdiag, float* toff, float* Vh,

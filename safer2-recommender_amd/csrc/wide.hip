@@ -44,6 +44,7 @@
 #include "chol.h"
 #include "common.h"
 #include "kernels.h"
+#include "wide.h"
 
 // waves per SIMD wide_chol_kernel<16> is compiled for (4: two workgroups per
 // CU, 128 registers, 30.5 ms at MSD; 2: one workgroup, 256 registers,
@@ -70,10 +71,6 @@ __device__ __forceinline__ void pair_of(int pidx, int& BI, int& BJ) {
   BJ = pidx - BI * (BI + 1) / 2;
 }
 
-__device__ __forceinline__ int64_t wide_virt_pos(int64_t k, int64_t h) {
-  return k < h ? k : (h - 128 + (k - h));
-}
-
 __device__ __forceinline__ float block_sum(float v, float* red) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -86,17 +83,6 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return s;
 }
 
-// XCD-aware grid: workgroup b runs on XCD b % 8 (round-robin dispatch), so
-// the P block pairs of one unit (entity / row block) are given consecutive
-// slots of ONE XCD's sequence -- they run together and the unit's rows are
-// fetched from HBM once into that XCD's L2 instead of once per pair.
-__device__ __forceinline__ bool xcd_unit(int P, int64_t n_units, int64_t& unit, int& pidx) {
-  const int64_t bid = blockIdx.x;
-  const int64_t s = bid >> 3;
-  pidx = (int)(s % P);
-  unit = (s / P) * 8 + (bid & 7);
-  return unit < n_units;
-}
 
 // ---- SYRK of A (MODE 1) / partial Gramians (MODE 0) over 256 x 256 block
 // pairs, fp32 products on the bf16 matrix cores ----
@@ -1470,7 +1456,6 @@ __global__ void __launch_bounds__(256) loss_gather_wide_kernel(LossArgs a) {
   if (lane == 0) a.out[e] = loss;
 }
 
-unsigned xcd_grid(int64_t n_units, int P) { return (unsigned)(((n_units + 7) / 8) * 8 * P); }
 
 size_t wide_chol_lds_bytes(int Dp) {
   const int T = Dp >> 5;
@@ -1522,7 +1507,7 @@ hipError_t launch_wide_gram_final(int Dp, const float* gslabs, int64_t ngroup, f
 }
 
 hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batch,
-                             hipStream_t s) {
+                             hipStream_t s, char* xsplit) {
   if (!wide_dim(Dp) || batch <= 0) return hipErrorInvalidValue;
   if (a.n_rows <= 0) return hipSuccess;
   const bool off64 = gather_off64(a.n_other, Dp);
@@ -1540,8 +1525,21 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
   }
   const bool grad = is_grad_kind(a.kind);
   GramArgs g{};
+  // the SYRK from the pre-split table (wide_syrk.hip; xsplit: its buffer,
+  // wide_xsplit_bytes), or the register-staged wide_syrk2_kernel (nullptr)
+  SolveArgs a3 = a;
+  if (xsplit) {
+    hipError_t e = launch_wide_presplit(Dp, a, xsplit, s);
+    if (e != hipSuccess) return e;
+    a3.xsplit = xsplit;
+    if (a.n_work > 0) {
+      if (a.n_split > std::min<int64_t>(batch, a.n_rows)) return hipErrorInvalidValue;
+      e = launch_wide_syrk3(Dp, a3, 2, 0, a.n_work, ws, s);
+      if (e != hipSuccess) return e;
+    }
+  }
   // the slabs of the long histories (all in the first batch) first
-  if (a.n_work > 0) {
+  if (a.n_work > 0 && !xsplit) {
     if (a.n_split > std::min<int64_t>(batch, a.n_rows)) return hipErrorInvalidValue;
     if (off64)
       hipLaunchKernelGGL((wide_syrk2_kernel<2, true>), dim3(xcd_grid(a.n_work, wide_pairs2(Dp))),
@@ -1552,7 +1550,10 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
   }
   for (int64_t s0 = 0; s0 < a.n_rows; s0 += batch) {
     const int64_t nb = std::min<int64_t>(batch, a.n_rows - s0);
-    if (off64)
+    if (xsplit) {
+      hipError_t e = launch_wide_syrk3(Dp, a3, 1, s0, nb, ws, s);
+      if (e != hipSuccess) return e;
+    } else if (off64)
       hipLaunchKernelGGL((wide_syrk2_kernel<1, true>), dim3(xcd_grid(nb, wide_pairs2(Dp))),
                          dim3(512), 0, s, a, g, Dp, (int64_t)0, s0, ws, nb);
     else

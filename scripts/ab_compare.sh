@@ -6,6 +6,7 @@ mkdir -p $OUT
 LIB=safer2-recommender_amd/frecsys_hip/libfrecsys_hip.so
 cp $LIB $OUT/base.so.bak
 restore() { cp $OUT/base.so.bak $LIB; }
+trap restore EXIT
 for v in $VS; do
   cp ab/libfrecsys_hip_$v.so $LIB
   timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_parity_gpu.py tests/test_dual_gpu.py tests/test_split_gpu.py tests/test_models_gpu.py > $OUT/pytest_$v.log 2>&1; rc=$?
