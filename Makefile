@@ -31,6 +31,9 @@ oracle: $(ORACLE)
 run_model: $(RUNMODEL)
 model_dump: $(MODELDUMP)
 
+# the wide SYRK: no SLP pairing of its scalar f32 subtractions (v_pk_add_f32
+# beside MFMAs costs issue cycles)
+$(OBJ)/wide_syrk.o ab/obj/wide_syrk.o: HIPFLAGS += -fno-slp-vectorize
 $(OBJ)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
