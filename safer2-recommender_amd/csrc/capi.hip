@@ -143,8 +143,8 @@ struct frecsys_ctx {
   size_t cap_topk = 0;
   float* wide_ws = nullptr;      // [wide batch][wide_slot_floats(Dp)]
   size_t cap_wide_ws = 0;
-  // the rows buffer of the wide d-space SYRK (wide.h wide_xsplit_bytes;
-  // FRECSYS_WIDE_PRESPLIT=0: the register-staged SYRK of wide.hip)
+  // the pre-split copy of the other side for the wide d-space SYRK
+  // (wide_syrk.hip; FRECSYS_WIDE_PRESPLIT=0: the register-staged SYRK)
   char* wide_xs = nullptr;
   size_t cap_wide_xs = 0;
   bool wide_presplit = true;
@@ -1430,9 +1430,7 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
     ap.prof = wprof ? w_prof : nullptr;
     char* xs = nullptr;
     if (c->wide_presplit && ap.n_rows > 0) {
-      rc = ensure(c, &c->wide_xs, &c->cap_wide_xs,
-                  wide_xsplit_bytes(c->Dp, ap.n_other, ap.kind == FRECSYS_KIND_WEIGHTED_V ||
-                                                        ap.kind == FRECSYS_KIND_CVAR_GRAD_V));
+      rc = ensure(c, &c->wide_xs, &c->cap_wide_xs, wide_xsplit_bytes(c->Dp, ap.n_other));
       if (rc) return rc;
       xs = c->wide_xs;
     }

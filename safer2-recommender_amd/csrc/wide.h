@@ -38,15 +38,16 @@ inline unsigned xcd_grid(int64_t n_units, int P) {
 constexpr int kWideChunk = 16;
 constexpr int kWideFlush = 128;
 
-// ---- the rows of the wide d-space SYRK (wide_syrk.hip) ----
-// V kinds: a pre-scaled copy of the other side, row r = sqrt(nu_r) X[r]
-// ([n_other + 1][Dp] floats, row n_other zero), then the rhs weights
-// nu_r / sqrt(nu_r) ([n_other + 1] floats); the other kinds read X itself
-// and this buffer holds only the zero row (Dp floats).
-inline size_t wide_xsplit_bytes(int Dp, int64_t n_other, bool v_kind) {
-  return sizeof(float) * (v_kind ? (size_t)(n_other + 1) * (Dp + 1) : (size_t)Dp);
+// ---- the pre-split copy of the other side (wide_syrk.hip) ----
+// Row r: the three bf16 pieces (hi, mid, lo; common.h split3) of
+// x~ = sa_r * X[r] (sa_r = sqrt(nu_r) for the V kinds, else 1), each Dp
+// values, then a 128-B tail whose first float is the rhs weight nu_r / sa_r
+// (V kinds).  Row n_other is all zero: the rows past a unit's end read it.
+__host__ __device__ inline int64_t wide_xsplit_row_bytes(int Dp) { return 6 * (int64_t)Dp + 128; }
+inline size_t wide_xsplit_bytes(int Dp, int64_t n_other) {
+  return (size_t)(n_other + 1) * (size_t)wide_xsplit_row_bytes(Dp);
 }
-// The buffer above for a (the pre-scaled copy for the V kinds, else zeros).
+// The pre-split table of a.X (with a.other_weight for the V kinds) into xs.
 hipError_t launch_wide_presplit(int Dp, const SolveArgs& a, char* xs, hipStream_t s);
 // MODE 2: the long-history slabs a.work[0..n_work); MODE 1: entities
 // a.order[pos0 .. pos0 + n) into the workspace ws (a.xsplit set).
