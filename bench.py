@@ -76,10 +76,14 @@ WORKLOADS = {
     "safer2_2m500k_d1024": dict(
         config=4, model="safer2", shape="2m500k", dim=1024, readme="README.md:100",
         flags=dict(l2_reg=0.0012, uobs_weight=0.0004, alpha=0.3, bandwidth=0.1,
-                   pd_iterations=1, xi_iterations=5, use_snr=True, sampling_ratio=0.1)),
+                   pd_iterations=1, xi_iterations=5, use_snr=True, sampling_ratio=0.1),
+        max_extra_steps=2),  # ~1.6 s epochs after ~40 s of data generation
 }
 HEADLINE = "ials_ml20m_d256"
 DEFAULT_EXTRAS = ("safer2_ml20m_d256", "ials_msd_d512")
+# measured after the others on one GPU only (a strong-scaling N>1 run keeps
+# to the three smaller configs so the driver's scaling sweep stays short)
+DEFAULT_EXTRAS_N1 = ("safer2_2m500k_d1024",)
 
 
 def parse():
@@ -88,9 +92,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
-    ap.add_argument("--extras", default=",".join(DEFAULT_EXTRAS),
+    ap.add_argument("--extras", default=None,
                     help="comma-separated extra workloads measured after the headline "
-                         "('' for none)")
+                         "('' for none; default: the other BASELINE configs, the 2M x 500K "
+                         "d=1024 one at N=1 only)")
     ap.add_argument("--extra-steps", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU-baseline sample duration per workload (0 disables)")
@@ -429,9 +434,10 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
         "u_halfstep_solve_updates_per_s": ((uhi - ulo) / (su_ms * 1e-3)) * world if su_ms else None,
         "kernel_ms_per_epoch": {k: v[0] / max(K, 1) for k, v in timers.items()},
         "roofline": {"bound": "mfma",
-                     "kernel": ("wide_syrk2_kernel<2> (slabs of the long histories) + "
-                                "wide_syrk2_kernel<1> + wide_chol_kernel<16> (batched d-space "
-                                "solve, A in an HBM workspace)") if wide else
+                     "kernel": ("wide_syrk3_kernel<2> (slabs of the long histories) + "
+                                "wide_syrk3_kernel<1> (split-bf16 MFMA SYRK from the pre-split "
+                                "table) + wide_chol_kernel<16> (batched d-space solve, A in an "
+                                "HBM workspace)") if wide else
                                ("solve_tiled_kernel<8, false, true> (d-space solve: split-bf16 "
                                 "MFMA SYRK + fp32 dataflow Cholesky)"),
                      "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
@@ -508,9 +514,12 @@ def main():
     head = run_workload(args.workload, args, world, rank, local_rank, dist, data_cache,
                         args.steps, args.warmup, args.cpu_seconds)
     extras = []
+    if args.extras is None:
+        args.extras = ",".join(DEFAULT_EXTRAS + (DEFAULT_EXTRAS_N1 if world == 1 else ()))
     for name in [x for x in args.extras.split(",") if x and x != args.workload]:
+        steps = min(args.extra_steps, WORKLOADS[name].get("max_extra_steps", args.extra_steps))
         extras.append(run_workload(name, args, world, rank, local_rank, dist, data_cache,
-                                   args.extra_steps, 1, args.cpu_seconds))
+                                   steps, 1, args.cpu_seconds))
     if rank == 0:
         spec = WORKLOADS[args.workload]
         line = {

@@ -39,9 +39,11 @@ def loss_kernel(name):
 
 def dominant(name, workload):
     if "d512" in workload or "d1024" in workload:
-        # the batched d-space call: slab SYRK, entity SYRK and Cholesky launches
-        return any(k in name for k in ("wide_syrk2_kernel<1>", "wide_syrk2_kernel<2>",
-                                       "wide_chol_kernel"))
+        # the batched d-space call: the pre-split table, slab SYRK, entity
+        # SYRK and Cholesky launches (wide_syrk2: FRECSYS_WIDE_PRESPLIT=0)
+        return any(k in name for k in ("wide_presplit_kernel", "wide_syrk3_kernel<1",
+                                       "wide_syrk3_kernel<2", "wide_syrk2_kernel<1>",
+                                       "wide_syrk2_kernel<2>", "wide_chol_kernel"))
     return "solve_tiled_kernel<8, false" in name
 
 
