@@ -186,7 +186,6 @@ struct frecsys_ctx {
   // [key0, key1)).  At N ranks a shard's short histories touch a fraction of
   // the other side, so the replicated rotation shrinks with N.  Built once
   // per (queue, split point) -- the histories do not change between epochs.
-  int rot_subset_on = 1;            // FRECSYS_ROT_SUBSET=0: rotate every row (A/B)
   QueueRec* d_hrows[3] = {nullptr, nullptr, nullptr};
   size_t cap_hrows[3] = {0, 0, 0};
   int64_t n_hrows[3] = {-1, -1, -1};  // rows in the subset; -1: none (every row)
@@ -560,7 +559,7 @@ int hspace_rows(frecsys_ctx* c, int side, int other, int64_t q0, int64_t q1,
   *rows = nullptr;
   *nrows = 0;
   *sub = 0;
-  if (!c->rot_subset_on || q1 <= q0) return FRECSYS_OK;
+  if (q1 <= q0) return FRECSYS_OK;
   if (c->hrows_key[side][0] != q0 || c->hrows_key[side][1] != q1) {
     // an early build may still be rotating with the old list (stream5): the
     // synchronisation below then covers it before the list is rewritten
@@ -952,11 +951,9 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   }
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
     return bail(fail(c, FRECSYS_ERR_HIP, "hipEventCreate failed"));
-  int s3_pri = 0;  // FRECSYS_S3_PRIO=1: the second bucket lane / early builds at high priority
-  if (const char* v = getenv("FRECSYS_S3_PRIO"); v && atoi(v)) {
-    int lo_pri = 0;
-    (void)hipDeviceGetStreamPriorityRange(&lo_pri, &s3_pri);
-  }
+  // the second bucket lane / early builds at normal priority (high priority
+  // measured no better)
+  const int s3_pri = 0;
   if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithPriority(&c->stream3, hipStreamNonBlocking, s3_pri) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
@@ -977,7 +974,6 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
     return bail(fail(c, FRECSYS_ERR_HIP, "hipEventCreate failed (early builds)"));
   if (const char* v = getenv("FRECSYS_DUAL")) c->dual_on = atoi(v);
   if (const char* v = getenv("FRECSYS_EAGER")) c->eager_on = atoi(v);
-  if (const char* v = getenv("FRECSYS_ROT_SUBSET")) c->rot_subset_on = atoi(v);
   if (const char* v = getenv("FRECSYS_CHOL_BASIS")) c->chol_basis_on = atoi(v);
   // d-space / history-space crossover: by flops h = d, but at Dp <= 256 the
   // d-space kernel overtakes the TH = 8 bucket (225 < h <= 256) in time (epoch
@@ -1655,7 +1651,7 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       // reduction, no per-entity LDL
       int bmode = 0;
       float bmu = 0.f, blam = 0.f;
-      if (c->chol_basis_on && c->Dp <= 512 && kind == FRECSYS_KIND_IALS &&
+      if (c->chol_basis_on && kind == FRECSYS_KIND_IALS &&
           (p->lambda_is_reg || p->reg_exp == 0.0f)) {
         bmode = 1;
         bmu = p->unobserved_weight;
@@ -1840,13 +1836,9 @@ int frecsys_user_loss(frecsys_ctx* c, int32_t side, float beta, int32_t half, fl
     HIP_TRY(c, hipMemsetAsync(c->d_loss, 0, sizeof(float) * std::max<size_t>(rows, 1), c->stream));
   int64_t lo, hi;
   shard(c, side, &lo, &hi);
-  // Dp = 64..256: u^T G u by the rotation kernel (column-block partials) unless
-  // FRECSYS_QUAD_ROT=0 (quad_kernel, f32 MFMA; A/B)
-  static const bool quad_rot = [] {
-    const char* v = getenv("FRECSYS_QUAD_ROT");
-    return !v || atoi(v) != 0;
-  }();
-  const bool qr = !wide_dim(c->Dp) && c->Dp >= 64 && c->Dp % 32 == 0 && quad_rot;
+  // Dp = 64..256: u^T G u by the rotation kernel (column-block partials; it
+  // measured faster than quad_kernel's f32 MFMA, which keeps the other widths)
+  const bool qr = !wide_dim(c->Dp) && c->Dp >= 64 && c->Dp % 32 == 0;
   rc = ensure(c, &c->d_quad, &c->cap_quad,
               std::max<size_t>(wide_dim(c->Dp) ? wide_quad_floats(c->Dp, hi - lo)
                                : qr ? (size_t)rotate_quad_parts(c->Dp) * (size_t)(hi - lo)
@@ -1975,6 +1967,8 @@ int frecsys_pp_predict(frecsys_ctx* c, int32_t side) {
   if (!c->rp[side]) return fail(c, FRECSYS_ERR_INVALID, "pp_predict: no CSR");
   if (side == 0 && !c->d_rix[0])
     return fail(c, FRECSYS_ERR_INVALID, "pp_predict: no rating index (pp_set_rating_index)");
+  if (c->pp_old_side != -1)  // the other ranks' updates of the last block are not in yet
+    return fail(c, FRECSYS_ERR_INVALID, "pp_predict: pp_sync pending for the last sharded block step");
   HIP_TRY(c, hipSetDevice(c->device));
   if (side == 2) {
     int rc = ensure(c, &c->d_pred[1], &c->cap_pred[1], (size_t)std::max<int64_t>(c->nnz[2], 1));
@@ -2003,6 +1997,11 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
     return fail(c, FRECSYS_ERR_INVALID, "pp_step: kind must be IALS, WEIGHTED_U or WEIGHTED_V");
   if (kind == FRECSYS_KIND_WEIGHTED_V && (!p->entity_reg || !p->other_weight))
     return fail(c, FRECSYS_ERR_INVALID, "pp_step: WEIGHTED_V needs entity_reg and other_weight");
+  // external-exchange mode: a second step before frecsys_pp_sync would
+  // overwrite the snapshot the other ranks' prediction updates are replayed
+  // from, and this rank's predictions would drift from theirs
+  if (c->pp_old_side != -1)
+    return fail(c, FRECSYS_ERR_INVALID, "pp_step: pp_sync pending for the last sharded block step");
   HIP_TRY(c, hipSetDevice(c->device));
   const int other = side == 1 ? 0 : 1;
   {

@@ -5,42 +5,15 @@
 
 #include "common.h"
 
-// 1 (default): the d-space and history-space kernels factor with the
-// dataflow chol_solve_df; 0: the barrier-phased chol_solve_tiles.
-#ifndef FRECSYS_CHOL_DF
-#define FRECSYS_CHOL_DF 1
-#endif
-// 1 (default): diagonal blocks by diag_factor_inv_blk (MFMA cross terms).
-#ifndef FRECSYS_DIAG_BLK
-#define FRECSYS_DIAG_BLK 1
-#endif
-// 1: the dataflow Cholesky's TRSM and trailing-update tile products on the
-// bf16 matrix cores with 3-piece split operands (tile_pqT_x6), in the kernels
-// that run the blocked diagonal factor (BLK: the register budget for it).
-#ifndef FRECSYS_CHOL_X6
-#define FRECSYS_CHOL_X6 1
-#endif
 // With 8 waves: the wave that runs the forward substitution (Y, B of the
 // chain's next block).  Waves w and w + 4 share a SIMD, so 4 leaves the
 // chain wave's SIMD without a worker's tile products beside it.
-// n > 0: a worker raises its issue priority (1; the chain runs at 2) over
-// the worker that shares its SIMD for the panel-p tasks of block rows
-// I <= p + 1 + n -- n = 1: the ones that feed the chain's next block
+constexpr int kCholYWave = 4;
+// A worker raises its issue priority (1; the chain runs at 2) over the
+// worker that shares its SIMD for the panel-p tasks of block rows
+// I <= p + 1 + kCholWPrio -- the ones that feed the chain's next block
 // (S(p+2, p), U(p+2, p+1, p), U(p+2, p+2, p)).
-#ifndef FRECSYS_CHOL_WPRIO
-#define FRECSYS_CHOL_WPRIO 1
-#endif
-// 1: the chain's update of the next diagonal tile, U(p+1, p+1, p), stays
-// in registers and goes straight into its factor F(p+1) (the accumulator
-// layout turned into rows by v_permlane32_swap: the tile is symmetric), so
-// no LDS write + read-back of the tile sits on the chain.  Kernels with the
-// blocked factor and split-bf16 products only.
-#ifndef FRECSYS_CHOL_FUSE
-#define FRECSYS_CHOL_FUSE 1
-#endif
-#ifndef FRECSYS_CHOL_YWAVE
-#define FRECSYS_CHOL_YWAVE 4
-#endif
+constexpr int kCholWPrio = 1;
 
 namespace frecsys_hip {
 
@@ -67,55 +40,23 @@ __device__ __forceinline__ float rdlane(float v, int l) {
 typedef __attribute__((address_space(3))) float lds_float;
 
 // Lanes 0..31: row r of the swizzled tile; lanes 32..63: column r of the
-// identity.  The reads are issued G at a time before a wait (both halves
-// read: no divergent loads; the asm keeps the select below after the loads
-// instead of turning it into per-element branches).  G = 8 cuts the waits
-// 8x but holds 8 addresses; G = 1 for the register-capped callers.
-// Element (r, c) of a diagonal tile: the XOR swizzle sw(r, c) (LDP = 0), or
-// rows padded to LDP floats (LDP = 36: constant offsets from one base per
-// lane -- no per-element address registers -- and conflict-free row and
-// column access alike; solve_rr.hip).
-template <int LDP>
-__device__ __forceinline__ int tix(int r, int c) {
-  if constexpr (LDP == 0) return sw(r, c);
-  return r * LDP + c;
-}
-
-template <int G, int LDP = 0>
+// identity.  The row as 8 granule reads (conflict-free, see common.h sw);
+// G = 1: every value pinned in its own register before the select below
+// (the register-capped callers), else the select may be folded into the
+// loads' uses.  Both halves read: no divergent loads.
+template <int G>
 __device__ __forceinline__ void load_factor_rows(const lds_float* tile, int r, bool fl,
                                                  float (&a)[32]) {
-  if constexpr (FRECSYS_GSW && LDP == 0) {
-    // the row as 8 granule reads (conflict-free, see common.h sw)
-    typedef __attribute__((address_space(3))) const f32x4v lds_f32x4c;
+  typedef __attribute__((address_space(3))) const f32x4v lds_f32x4c;
 #pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      const f32x4v v = *reinterpret_cast<lds_f32x4c*>(tile + r * 32 + (((g ^ (r >> 1)) & 7) << 2));
+  for (int g = 0; g < 8; ++g) {
+    const f32x4v v = *reinterpret_cast<lds_f32x4c*>(tile + r * 32 + (((g ^ (r >> 1)) & 7) << 2));
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[4 * g + t] = v[t];
-    }
-    if constexpr (G == 1) {
-#pragma unroll
-      for (int c = 0; c < 32; ++c) asm volatile("" : "+v"(a[c]));
-    }
-#pragma unroll
-    for (int c = 0; c < 32; ++c) a[c] = fl ? a[c] : (c == r ? 1.0f : 0.0f);
-    return;
+    for (int t = 0; t < 4; ++t) a[4 * g + t] = v[t];
   }
   if constexpr (G == 1) {
 #pragma unroll
-    for (int c = 0; c < 32; ++c) {
-      float t = tile[tix<LDP>(r, c)];
-      asm volatile("" : "+v"(t));
-      a[c] = fl ? t : (c == r ? 1.0f : 0.0f);
-    }
-    return;
-  }
-#pragma unroll
-  for (int c0 = 0; c0 < 32; c0 += G) {
-#pragma unroll
-    for (int c = c0; c < c0 + G; ++c) a[c] = tile[tix<LDP>(r, c)];
-#pragma unroll
-    for (int c = c0; c < c0 + G; ++c) asm volatile("" : "+v"(a[c]));
+    for (int c = 0; c < 32; ++c) asm volatile("" : "+v"(a[c]));
   }
 #pragma unroll
   for (int c = 0; c < 32; ++c) a[c] = fl ? a[c] : (c == r ? 1.0f : 0.0f);
@@ -173,7 +114,6 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
 // MFMAs.
 // The factor from rows already in registers (a: lanes 0..31 row r of A,
 // lanes 32..63 column r of the identity); L^-1 goes to the tile.
-template <int LDP = 0>
 __device__ __forceinline__ bool diag_factor_inv_blk_regs(float (&a)[32], lds_float* tile,
                                                          int lane) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -247,24 +187,22 @@ __device__ __forceinline__ bool diag_factor_inv_blk_regs(float (&a)[32], lds_flo
     // (zero inputs times finite factors): stored as they are
 #pragma unroll
     for (int k = 0; k < 32; ++k)
-      if (!fl) tile[tix<LDP>(k, j)] = a[k];
+      if (!fl) tile[sw(k, j)] = a[k];
   } else {
 #pragma unroll
     for (int k = 0; k < 32; ++k)
-      if (!fl) tile[tix<LDP>(k, j)] = (k >= j) ? a[k] : 0.0f;
+      if (!fl) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
   }
   return ok;
 }
-template <int LDP = 0>
-__device__ __forceinline__ bool diag_factor_inv_blk_inl(lds_float* tile, int lane) {
-  float a[32];
-  load_factor_rows<8, LDP>(tile, lane & 31, lane < 32, a);
-  return diag_factor_inv_blk_regs<LDP>(a, tile, lane);
-}
 // The same from the chain's updated diagonal tile in MFMA accumulator layout
-// (c[q] = element (acc_row(q, hi), lo)): the tile is symmetric, so lane lo's
-// row lo is its own 16 values and lane lo+32's (one v_permlane32_swap each).
-// A call, as diag_factor_inv_blk (the accumulator travels in 16 VGPRs).
+// (c[q] = element (acc_row(q, hi), lo)): lane lo takes COLUMN lo of the
+// updated tile (its own 16 values and lane lo+32's, one v_permlane32_swap
+// each) as row lo.  The tile is symmetric in exact arithmetic only -- the
+// split-bf16 product's (i, j) and (j, i) terms accumulate in different
+// orders -- so this factors the transposed lower triangle and agrees with a
+// factor of the stored tile to rounding, not bitwise.  A call, as
+// diag_factor_inv_blk (the accumulator travels in 16 VGPRs).
 __device__ __noinline__ bool diag_factor_inv_acc(f32x16 c, lds_float* tile) {
   const int lane = __lane_id();
   const int r = lane & 31;
@@ -278,13 +216,13 @@ __device__ __noinline__ bool diag_factor_inv_acc(f32x16 c, lds_float* tile) {
     a[c0] = fl ? c[q] : (c0 == r ? 1.0f : 0.0f);
     a[c1] = fl ? __uint_as_float(sv[1]) : (c1 == r ? 1.0f : 0.0f);
   }
-  return diag_factor_inv_blk_regs<0>(a, tile, lane);
+  return diag_factor_inv_blk_regs(a, tile, lane);
 }
-// As a call: callers with few live registers (the tiled kernels); a caller
-// holding its matrix in registers (solve_rr.hip) inlines the body instead,
-// since a call clobbers half of the VGPRs and the live tiles would spill.
+// As a call: the register cost counts once, not per call site.
 __device__ __noinline__ bool diag_factor_inv_blk(lds_float* tile, int lane) {
-  return diag_factor_inv_blk_inl<0>(tile, lane);
+  float a[32];
+  load_factor_rows<8>(tile, lane & 31, lane < 32, a);
+  return diag_factor_inv_blk_regs(a, tile, lane);
 }
 
 // BLK = true for kernels with a register budget above ~150 VGPRs (the
@@ -292,7 +230,7 @@ __device__ __noinline__ bool diag_factor_inv_blk(lds_float* tile, int lane) {
 // toward the caller's allocation, so a capped kernel would lose occupancy).
 template <bool BLK = false>
 __device__ __forceinline__ bool diag_factor_inv(float* tile, int lane) {
-  if constexpr (BLK && FRECSYS_DIAG_BLK) return diag_factor_inv_blk((lds_float*)tile, lane);
+  if constexpr (BLK) return diag_factor_inv_blk((lds_float*)tile, lane);
   return diag_factor_inv_lds((lds_float*)tile, lane);
 }
 
@@ -301,17 +239,12 @@ __device__ __forceinline__ bool diag_factor_inv(float* tile, int lane) {
 // one b128 read of row lo's columns 4g .. 4g+3 serves s = 2g and 2g + 1.
 __device__ __forceinline__ f32x16 tile_pqT(const float* P, const float* Q, int lo, int hi) {
   f32x16 u = f32x16{0.f};
-#if FRECSYS_GSW
 #pragma unroll
   for (int g = 0; g < 8; ++g) {
     const f32x4v pv = row_gran(P, lo, g), qv = row_gran(Q, lo, g);
     u = mfma32(hi ? pv[1] : pv[0], hi ? qv[1] : qv[0], u);
     u = mfma32(hi ? pv[3] : pv[2], hi ? qv[3] : qv[2], u);
   }
-#else
-#pragma unroll
-  for (int s = 0; s < 16; ++s) u = mfma32(P[sw(lo, 2 * s + hi)], Q[sw(lo, 2 * s + hi)], u);
-#endif
   return u;
 }
 
@@ -326,7 +259,6 @@ __device__ __forceinline__ f32x16 tile_pqT_x6(const float* P, const float* Q, in
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     float pv[8], qv[8];
-#if FRECSYS_GSW
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
       const f32x4v p4 = row_gran(P, lo, 4 * g + 2 * hi + h2);
@@ -338,13 +270,6 @@ __device__ __forceinline__ f32x16 tile_pqT_x6(const float* P, const float* Q, in
         for (int t = 0; t < 4; ++t) qv[4 * h2 + t] = q4[t];
       }
     }
-#else
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      pv[j] = P[sw(lo, 16 * g + 8 * hi + j)];
-      if (!SAME) qv[j] = Q[sw(lo, 16 * g + 8 * hi + j)];
-    }
-#endif
     bf16x8 pf[3], qf[3];
     split3x8(pv, pf);
     if (SAME) {
@@ -358,8 +283,9 @@ __device__ __forceinline__ f32x16 tile_pqT_x6(const float* P, const float* Q, in
 }
 
 // ---------------------------------------------------------------------
-// Solve A x = b for the SPD matrix whose lower T(T+1)/2 tiles sit in LDS
-// (tile (I, J) at tiles + tidx(I, J) * 1024, swizzled), NW waves.
+// Barrier-phased solve (pp.hip's block steps, TB <= 4 tiles): A x = b for
+// the SPD matrix whose lower T(T+1)/2 tiles sit in LDS (tile (I, J) at
+// tiles + tidx(I, J) * 1024, swizzled), NW waves.
 //
 // Right-looking blocked Cholesky with lookahead: diagonal tiles become
 // L_pp^-1 (diag_factor_inv); the panel TRSM is an MFMA product with
@@ -475,9 +401,16 @@ __device__ __forceinline__ void chol_solve_tiles(float* tiles, float* bvec, floa
 }
 
 // ---------------------------------------------------------------------
-// Dataflow variant of chol_solve_tiles (same inputs, outputs and scratch
-// contract; part[] must hold 2T + T(T+1)/2 + 2 ints and 32 floats).  The
-// blocked factorisation and both substitutions are tile tasks
+// Dataflow solve (the d-space and history-space kernels): A x = b for the
+// SPD matrix whose lower T(T+1)/2 tiles sit in LDS (tile (I, J) at
+// tiles + tidx(I, J) * 1024, swizzled), NW waves.
+// In: tiles, bvec[32T] = b, a barrier since they were written.
+// Out: xvec[32T] = x; bvec = y; *flag = 1 on a non-positive pivot; the
+// diagonal tiles hold L_pp^-1.  Scratch: part[] holds 2T + T(T+1)/2 + 2
+// ints and 32 floats.  Ends with a barrier.
+// Blocked Cholesky with the diagonal tiles inverted (the panel TRSM is an
+// MFMA product with L_pp^-1); the factorisation and both substitutions are
+// tile tasks
 //   F(p)      factor + invert diagonal tile (p, p)
 //   Y(p)      y_p = L_pp^-1 b_p                       (b_p fully updated)
 //   S(I, p)   TRSM  L_Ip = A_Ip (L_pp^-1)^T                       (I > p)
@@ -524,7 +457,7 @@ __device__ __forceinline__ void set_ver(int* f, int v, int lane) {
 template <bool TR>
 __device__ __forceinline__ float tile_gemv(const float* M, const float* v, int lo, int hi) {
   float s0 = 0.0f, s1 = 0.0f;
-  if constexpr (!TR && FRECSYS_GSW) {
+  if constexpr (!TR) {
     // row lo's columns 16 hi .. +15 as four granule reads
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -553,9 +486,11 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
                                               unsigned long long* prof = nullptr) {
   static_assert(NW >= 2, "one chain wave and at least one worker");
   constexpr int NT = T * (T + 1) / 2;
-  // split-bf16 tile products where the register budget allows (as BLK)
-  constexpr bool X6 = FRECSYS_CHOL_X6 && BLK;
-  constexpr bool FUSE = FRECSYS_CHOL_FUSE && X6 && FRECSYS_DIAG_BLK;
+  // split-bf16 tile products (common.h mfma_x6, fp32-accurate) where the
+  // register budget allows the blocked diagonal factor (BLK), and then the
+  // chain's next diagonal update fused into its factor (diag_factor_inv_acc)
+  constexpr bool X6 = BLK;
+  constexpr bool FUSE = BLK;
   const unsigned long long t0 = prof ? clock64() : 0;
   const int lane = tid & 63, lo = lane & 31, hi = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -613,7 +548,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
   // with 8 waves the forward substitution (Y, and B of the next block) runs
   // on its own wave behind the chain instead of on it
   constexpr bool YW = NW >= 8;
-  constexpr int YWAVE = YW ? FRECSYS_CHOL_YWAVE : -1;
+  constexpr int YWAVE = YW ? kCholYWave : -1;
   constexpr int NWK = YW ? NW - 2 : NW - 1;  // worker waves
   // worker slot s (0 .. NWK-1) -> wave: every wave but 0 and YWAVE, in order
   auto wk_wave = [&](int s) { return YW ? s + 1 + (s + 1 >= YWAVE ? 1 : 0) : s + 1; };
@@ -718,7 +653,7 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
         if (wk_wave(k % NWK) != wave) continue;
         wwait(ver + tidx(p, p), p + 1);
         wwait(ver + tidx(I, p), p);
-        if (FRECSYS_CHOL_WPRIO) wprio(I <= p + 1 + FRECSYS_CHOL_WPRIO);
+        wprio(I <= p + 1 + kCholWPrio);
         trsm(I, p);
         wwait(yver, p + 1);
         bupd(I, p);
@@ -731,12 +666,12 @@ __device__ __forceinline__ void chol_solve_df(float* tiles, float* bvec, float* 
           wwait(ver + tidx(I, p), p + 1);
           wwait(ver + tidx(J, p), p + 1);
           wwait(ver + tidx(I, J), p);
-          if (FRECSYS_CHOL_WPRIO) wprio(I <= p + 1 + FRECSYS_CHOL_WPRIO);
+          wprio(I <= p + 1 + kCholWPrio);
           update(I, J, p);
         }
       }
     }
-    if (FRECSYS_CHOL_WPRIO) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
     if (prof && lane == 0) {
       atomicAdd(prof + 6, (clock64() - t0) / NWK);
       atomicAdd(prof + 15, tww / NWK);

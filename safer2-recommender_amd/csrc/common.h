@@ -39,34 +39,21 @@ __host__ __device__ __forceinline__ bool is_grad_kind(int k) {
 // Tile (I, J), I >= J, of a T x T lower block layout.
 __host__ __device__ constexpr int tidx(int I, int J) { return I * (I + 1) / 2 + J; }
 
-// 32x32 fp32 tile in LDS.  FRECSYS_GSW = 1 (default): 16-B granules
-// XOR-swizzled per row pair -- element (r, c) at r*32 + 4 ((c/4) ^ (r/2 % 8))
-// + c % 4 -- so that a lane reading 4 consecutive columns of ITS row (lanes
-// over rows: the MFMA operand reads, the diagonal factor's row loads) issues
-// one conflict-free ds_read_b128 (row_gran: the 16 lanes of each b128 lane
-// group cover 16 distinct bank quads), and scalar accesses with lanes over
-// the columns of one row (the accumulator-layout stores) stay conflict-free.
-// 0: the element XOR swizzle r*32 + (c ^ r) (both scalar directions
-// conflict-free, no vector row reads).
-#ifndef FRECSYS_GSW
-#define FRECSYS_GSW 1
-#endif
+// 32x32 fp32 tile in LDS: 16-B granules XOR-swizzled per row pair --
+// element (r, c) at r*32 + 4 ((c/4) ^ (r/2 % 8)) + c % 4 -- so that a lane
+// reading 4 consecutive columns of ITS row (lanes over rows: the MFMA operand
+// reads, the diagonal factor's row loads) issues one conflict-free
+// ds_read_b128 (row_gran: the 16 lanes of each b128 lane group cover 16
+// distinct bank quads), and scalar accesses with lanes over the columns of
+// one row (the accumulator-layout stores) stay conflict-free.  (The element
+// swizzle r*32 + (c ^ r) it replaced, no vector row reads, was slower.)
 __device__ __forceinline__ int sw(int r, int c) {
-#if FRECSYS_GSW
   return r * 32 + ((((c >> 2) ^ (r >> 1)) & 7) << 2) + (c & 3);
-#else
-  return r * 32 + (c ^ r);
-#endif
 }
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 // Columns 4G .. 4G+3 of row r of a swizzled tile.
 __device__ __forceinline__ f32x4v row_gran(const float* tile, int r, int G) {
-#if FRECSYS_GSW
   return *reinterpret_cast<const f32x4v*>(tile + r * 32 + (((G ^ (r >> 1)) & 7) << 2));
-#else
-  return f32x4v{tile[sw(r, 4 * G)], tile[sw(r, 4 * G + 1)], tile[sw(r, 4 * G + 2)],
-                tile[sw(r, 4 * G + 3)]};
-#endif
 }
 
 // Row of a 32x32x2 f32 MFMA accumulator register q for a lane half `hi`
@@ -109,17 +96,11 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
-#ifdef FRECSYS_CHEAP_SPLIT  // timing ablation only (wrong numbers): the split's VALU cost
-  h = (__bf16)x;
-  m = (__bf16)0.0f;
-  l = (__bf16)0.0f;
-#else
   h = (__bf16)x;
   float r = x - (float)h;
   m = (__bf16)r;
   r -= (float)m;
   l = (__bf16)r;
-#endif
 }
 
 __device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {

@@ -32,7 +32,7 @@
 //     accumulate their S tiles while the next slab's loads are in flight --
 //     by default on the bf16 matrix cores with fp32-accurate 3-piece split
 //     operands (common.h mfma_x6), FRECSYS_SYRK_F32=1: v_mfma_f32_32x32x2_f32;
-//   * S tiles go to LDS (aliasing the slab buffers), chol_solve_tiles, then
+//   * S tiles go to LDS (aliasing the slab buffers), chol_solve_df, then
 //     Y^T (c.*z) re-reads the (cache-resident) rows with float4 loads.
 #include <hip/hip_runtime.h>
 
@@ -203,9 +203,7 @@ __global__ void __launch_bounds__(256) dual_sweep_kernel(DualArgs a) {
 
 // Smallest bucket whose Cholesky runs the blocked diagonal factor and the
 // split-bf16 tile products (chol.h BLK).
-#ifndef FRECSYS_DUAL_BLK_TH
-#define FRECSYS_DUAL_BLK_TH 3
-#endif
+constexpr int kDualBlkTH = 3;
 
 template <int TH, bool BF>
 __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
@@ -468,16 +466,12 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
   }
   lds_barrier();
   mark(1);
-#if FRECSYS_CHOL_DF
   // the MFMA-blocked diagonal factor where the register budget allows it
   // (every bucket since the granule tile layout: TH = 4, 5 keep their
   // occupancy without spills; TH = 3 at 128 registers spills 8, measured
   // faster all the same)
-  chol_solve_df<TH, NW, (TH >= FRECSYS_DUAL_BLK_TH)>(tiles, bvec, xvec, part, flag, tid,
-                                                     a.debug_skip, a.prof);
-#else
-  chol_solve_tiles<TH, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
-#endif
+  chol_solve_df<TH, NW, (TH >= kDualBlkTH)>(tiles, bvec, xvec, part, flag, tid, a.debug_skip,
+                                            a.prof);
   mark(2);
 
   // ---- v = Y^T (c.*z): the rows again, float4 per lane, 8 rows in flight ----
@@ -535,14 +529,9 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
 // ---------------------------------------------------------------------
 __device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
 
-// 1: the one-wave solve runs the blocked diagonal factor and split-bf16
-// tile products (chol.h) instead of the plain factor and f32 MFMA.
-#ifndef FRECSYS_WAVE_X6
-#define FRECSYS_WAVE_X6 1
-#endif
-
-// chol_solve_tiles for one wave (T <= 2): x = S^-1 b, S's lower tiles in
-// LDS (swizzled), diagonal tiles become L_pp^-1.
+// The Cholesky solve for one wave (T <= 2): x = S^-1 b, S's lower tiles in
+// LDS (swizzled), diagonal tiles become L_pp^-1; the blocked diagonal
+// factor and split-bf16 tile products (chol.h).
 template <int T>
 __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float* xvec,
                                                 int* flag, int lane, int debug_skip) {
@@ -551,7 +540,7 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
 #pragma unroll
   for (int p = 0; p < T; ++p) {
     float* Tpp = tiles + tidx(p, p) * 1024;
-    if (!FRECSYS_SKIP(debug_skip, 2) && !diag_factor_inv<FRECSYS_WAVE_X6>(Tpp, lane) && lane == 0)
+    if (!FRECSYS_SKIP(debug_skip, 2) && !diag_factor_inv<true>(Tpp, lane) && lane == 0)
       flag[0] = 1;
     wave_sync();
     // y_p = L_pp^-1 b_p  (lane lo, both halves compute, half 0 keeps it)
@@ -566,8 +555,7 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
     if (hi == 0) xvec[32 * p + lo] = yp;  // y staged for the panel update
     if (p + 1 < T) {
       float* A10 = tiles + tidx(p + 1, p) * 1024;
-      const f32x16 u = FRECSYS_WAVE_X6 ? tile_pqT_x6(A10, Tpp, lo, hi)
-                                       : tile_pqT(A10, Tpp, lo, hi);  // L_10 = A_10 L_00^-T
+      const f32x16 u = tile_pqT_x6(A10, Tpp, lo, hi);  // L_10 = A_10 L_00^-T
       wave_sync();
 #pragma unroll
       for (int q = 0; q < 16; ++q) A10[sw(acc_row(q, hi), lo)] = u[q];
@@ -580,8 +568,7 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
 #pragma unroll
         for (int u = 0; u < 4; ++u) t += x4[u] * xvec[32 * p + 4 * g + u];
       }
-      const f32x16 w = FRECSYS_WAVE_X6 ? tile_pqT_x6<true>(A10, A10, lo, hi)
-                                       : tile_pqT(A10, A10, lo, hi);
+      const f32x16 w = tile_pqT_x6<true>(A10, A10, lo, hi);
       float* A11 = tiles + tidx(p + 1, p + 1) * 1024;
       wave_sync();
       if (hi == 0) bvec[32 * (p + 1) + lo] -= t;

@@ -43,9 +43,7 @@
 // kernel 1.059 vs 1.086 ms/epoch; in the solve kernel the five ownership
 // copies of the SYRK loop spill beside the Cholesky's registers (2.72 vs 2.21
 // ms), so it keeps t % 8 there.
-#ifndef FRECSYS_SYRK_SB
-#define FRECSYS_SYRK_SB 1
-#endif
+constexpr int kSyrkSB = 1;
 
 namespace frecsys_hip {
 
@@ -148,7 +146,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
     solve_tiled_kernel(SolveArgs a) {
   using C = TiledCfg<T, BF>;
   // SB: super-block tile ownership (sb_tile) for the split-bf16 SYRK at T = 8
-  constexpr bool SB = BF && T == 8 && (FRECSYS_SYRK_SB >= 2 || (PARTIAL && FRECSYS_SYRK_SB >= 1));
+  constexpr bool SB = BF && T == 8 && (kSyrkSB >= 2 || (PARTIAL && kSyrkSB >= 1));
   constexpr int Dp = C::Dp, NT = C::NT, NW = C::NW, NTHR = C::NTHR;
   constexpr int MT = C::MT;
   constexpr int R = C::R, NQ = C::NQ, NSLOT = C::NSLOT;
@@ -723,11 +721,7 @@ __global__ void __launch_bounds__((TiledCfg<T, BF>::NTHR))
   }
 
   // ---- blocked right-looking Cholesky with lookahead + back-solve ----
-#if FRECSYS_CHOL_DF
   chol_solve_df<T, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip, a.prof);
-#else
-  chol_solve_tiles<T, NW>(tiles, bvec, xvec, part, flag, tid, a.debug_skip);
-#endif
   mark(3);
   if (tid < Dp) a.out[e * Dp + tid] = xvec[tid];
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));

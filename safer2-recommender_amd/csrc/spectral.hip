@@ -586,6 +586,8 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---- Cholesky basis: one M for every entity of the launch ----
+constexpr int chol_basis_stage_tiles(int T) { return T <= 16 ? 16 : 7; }
+
 // When every entity of a history-space launch has the same
 // M = mu*G + lam*I (iALS with l2_reg_exp = 0: RegularizationValue,
 // ials.h:310-315, is reg whatever the history; mu = unobserved_weight), the
@@ -599,7 +601,9 @@ __global__ void __launch_bounds__(256)
 //    trailing A_ij -= L_ip L_jp^T are f32 MFMA tile products (tile_pqT) over
 //    LDS copies, one tile per wave;
 //  * XT = L^-T by block rows of L: XT_ji = -(sum_{k=j}^{i-1} XT_jk L_ik^T)
-//    L_ii^-T (X = L^-1: L_ii X_ij = -sum_k L_ik X_kj), XT_ii = L_ii^-T.
+//    L_ii^-T (X = L^-1: L_ii X_ij = -sum_k L_ik X_kj), XT_ii = L_ii^-T, one
+//    tile j per wave of the first NS (16; 7 at Dp = 1024, where the panel of
+//    31 tiles leaves room for 7 staging tiles in the 160 KB of LDS).
 // status[0] = 1 when every pivot was positive, else 0 (dual_ldl_kernel turns
 // 0 into the launch's failure flag: the call reruns on the d-space path).
 template <int T>
@@ -607,11 +611,12 @@ __global__ void __launch_bounds__(1024)
     chol_basis_kernel(const float* __restrict__ G, float mu, float lam, float* __restrict__ A,
                       float* __restrict__ dinv, float* __restrict__ XT,
                       float* __restrict__ status) {
-  constexpr int Dp = 32 * T, NW = 16;
+  constexpr int Dp = 32 * T, NW = 16, NS = chol_basis_stage_tiles(T);
+  static_assert(NS < NW || T <= NW, "wave NW - 1 (XT's diagonal tiles) takes no tile j < T - 1");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* panel = sm;               // [T-1] swizzled tiles: panel p / block row i of L
   float* D = sm + (T - 1) * 1024;  // L_pp^-1, swizzled
-  float* stg = D + 1024;           // [NW] per-wave staging tile
+  float* stg = D + 1024;           // [NS] per-wave staging tile
   __shared__ int fail;
   const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -681,13 +686,13 @@ __global__ void __launch_bounds__(1024)
     }
     D[tid] = dinv[i * 1024 + tid];
     __syncthreads();
-    if (wave == NW - 1) {  // XT_ii = L_ii^-T (j < i <= T - 1 < NW - 1 never uses this wave)
+    if (wave == NW - 1) {  // XT_ii = L_ii^-T (the tiles j < i go to waves < NS < NW - 1)
       for (int e = lane; e < 1024; e += 64) {
         const int r = e >> 5, c = e & 31;
         XT[(32 * i + c) * Dp + 32 * i + r] = D[sw(r, c)];
       }
     }
-    for (int j = wave; j < i; j += NW) {
+    for (int j = wave; wave < NS && j < i; j += NS) {
       f32x16 acc = f32x16{0.f};
       for (int k = j; k < i; ++k) {  // C^T = sum_k XT_jk L_ik^T
         const float* src = XT + (32 * j + lo) * Dp + 32 * k + hi;
@@ -717,7 +722,7 @@ __global__ void __launch_bounds__(1024)
 template <int T>
 hipError_t launch_chol_basis_t(const float* G, float mu, float lam, float* work, float* XT,
                                float* status, hipStream_t s) {
-  const size_t lds = (size_t)(T + 16) * 1024 * sizeof(float);
+  const size_t lds = (size_t)(T + chol_basis_stage_tiles(T)) * 1024 * sizeof(float);
   static bool attr = false;
   if (!attr) {
     hipError_t err = hipFuncSetAttribute((const void*)chol_basis_kernel<T>,
@@ -839,33 +844,19 @@ __global__ void __launch_bounds__(256)
     }
 }
 
-// FRECSYS_ROT_RT (A/B): 0 = rotate_kernel, 1 / 2 = rotate_rt_kernel row tiles
-// per wave.  (An LDS-staged GEMM form -- X block split once per workgroup,
-// B's image copied to LDS, 128 x 128 blocks, two stages -- measured 2.97 ms,
-// slower: one workgroup per CU did not hide the loads.)  Default 2: 1.95 vs 2.20 ms for the 471,355 x 512 rotation, 0.138
-// vs 0.141 ms for 116,677 x 256, bit-identical (scripts/micro/rotate_bench.cpp)
-int rotate_rt() {
-  const char* v = getenv("FRECSYS_ROT_RT");
-  return v ? atoi(v) : 2;
-}
-int rotate_p() {  // 4 measured no better than 2 (scripts/micro/rotate_bench.cpp)
-  const char* v = getenv("FRECSYS_ROT_P");
-  return v ? atoi(v) : 2;
-}
-
+// rotate_rt_kernel with 2 row tiles per wave and P = 2 k-steps of loads in
+// flight: 1.95 vs 2.20 ms (rotate_kernel) for the 471,355 x 512 rotation,
+// 0.138 vs 0.141 ms for 116,677 x 256, bit-identical; RT = 1 and P = 4
+// measured no better (scripts/micro/rotate_bench.cpp).  (An LDS-staged GEMM
+// form -- X block split once per workgroup, B's image copied to LDS, 128 x
+// 128 blocks, two stages -- measured 2.97 ms: one workgroup per CU did not
+// hide the loads.)  rotate_kernel remains for the rotations that also form
+// the u^T G u partials.
 template <int DP, int RT>
 void launch_rotate_rtp(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
-                       const bf16x8* Bs, float* Y, hipStream_t s, int xb, int ncb, int p) {
+                       const bf16x8* Bs, float* Y, hipStream_t s, int xb, int ncb) {
   const int64_t units = (n + 64 * RT - 1) / (64 * RT);
   const unsigned grid = (unsigned)(((units + 7) / 8) * 8 * ncb);
-  constexpr int NS = DP / 16;
-  if constexpr (NS % 4 == 0) {
-    if (p == 4) {
-      hipLaunchKernelGGL((rotate_rt_kernel<DP, RT, 4>), dim3(grid), dim3(256), 0, s, X, rows, r0,
-                         n, Bs, Y, xb, ncb);
-      return;
-    }
-  }
   hipLaunchKernelGGL((rotate_rt_kernel<DP, RT, 2>), dim3(grid), dim3(256), 0, s, X, rows, r0, n,
                      Bs, Y, xb, ncb);
 }
@@ -876,12 +867,8 @@ hipError_t launch_rotate_t(const float* X, const QueueRec* rows, int64_t r0, int
                            float* qpart = nullptr) {
   constexpr int CBc = (DP % 128 == 0) ? 4 : 2;
   const int ncbc = (DP / 32 + CBc - 1) / CBc;
-  const int rt = qpart ? 0 : rotate_rt();
-  if (rt == 1 || rt == 2) {
-    if (rt == 1)
-      launch_rotate_rtp<DP, 1>(X, rows, r0, n, Bs, Y, s, xb, ncbc, rotate_p());
-    else
-      launch_rotate_rtp<DP, 2>(X, rows, r0, n, Bs, Y, s, xb, ncbc, rotate_p());
+  if (!qpart) {
+    launch_rotate_rtp<DP, 2>(X, rows, r0, n, Bs, Y, s, xb, ncbc);
     return hipGetLastError();
   }
   constexpr int CB = (DP % 128 == 0) ? 4 : 2;
@@ -895,13 +882,10 @@ hipError_t launch_rotate_t(const float* X, const QueueRec* rows, int64_t r0, int
 
 }  // namespace
 
-bool qpipe_on() {  // FRECSYS_QPIPE=0: form Q by form_q_kernel after the reduction (A/B)
-  const char* v = getenv("FRECSYS_QPIPE");
-  return !v || atoi(v) != 0;
-}
-
 bool tridiag_forms_q(int Dp) {
-  if (!qpipe_on() || Dp < 64 || Dp % 32) return false;
+  // Q rows (and their split images) formed inside the reduction's launch; a
+  // separate form_q_kernel launch after it measured slower
+  if (Dp < 64 || Dp % 32) return false;
   return wide_dim(Dp) ? wide_tridiag_tagged() : Dp <= 256;
 }
 
@@ -961,6 +945,7 @@ hipError_t launch_chol_basis(const float* G, int Dp, float mu, float lam, float*
     case 224: return launch_chol_basis_t<7>(G, mu, lam, work, XT, status, s);
     case 256: return launch_chol_basis_t<8>(G, mu, lam, work, XT, status, s);
     case 512: return launch_chol_basis_t<16>(G, mu, lam, work, XT, status, s);
+    case 1024: return launch_chol_basis_t<32>(G, mu, lam, work, XT, status, s);
     default: return hipErrorInvalidValue;
   }
 }

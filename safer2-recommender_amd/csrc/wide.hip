@@ -49,9 +49,7 @@
 // waves per SIMD wide_chol_kernel<16> is compiled for (4: two workgroups per
 // CU, 128 registers, 30.5 ms at MSD; 2: one workgroup, 256 registers,
 // 32.1 ms); at Dp = 1024 row p of L alone takes 128 KB of LDS: 2.
-#ifndef FRECSYS_WIDE_CHOL_WPE
-#define FRECSYS_WIDE_CHOL_WPE 4
-#endif
+constexpr int kWideCholWPE = 4;
 
 namespace frecsys_hip {
 
@@ -107,11 +105,8 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // every W2FLUSH chunks).
 constexpr int WB2 = 256;
 constexpr int W2R = 16;
-// rows gathered W2AH chunks ahead of their staging (FRECSYS_W2_AH, 1 or 2)
-#ifndef FRECSYS_W2_AH
-#define FRECSYS_W2_AH 2
-#endif
-constexpr int W2AH = FRECSYS_W2_AH;
+// rows gathered W2AH chunks ahead of their staging (1: measured slower)
+constexpr int W2AH = 2;
 static_assert(W2AH == 1 || W2AH == 2, "one or two chunks ahead");
 constexpr int W2RING = W2AH == 1 ? 4 : 8;
 constexpr int W2FLUSH = 128;
@@ -741,7 +736,7 @@ __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, fl
 // one 30.5 ms).  Compiled for two workgroups per CU (128 registers).
 template <int T>
 __global__ void __launch_bounds__(512)
-    __attribute__((amdgpu_waves_per_eu(T == 16 ? FRECSYS_WIDE_CHOL_WPE : 2, 8)))
+    __attribute__((amdgpu_waves_per_eu(T == 16 ? kWideCholWPE : 2, 8)))
     wide_chol_kernel(SolveArgs a, int64_t pos0, float* ws) {
   constexpr int Dp = 32 * T, NT = T * (T + 1) / 2, NW = 8;
   typedef float f32x4v __attribute__((ext_vector_type(4)));

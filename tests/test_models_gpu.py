@@ -56,8 +56,8 @@ CASES = {
     "safer2_snr": (O.MODEL_SAFER2, 0.004, 0.004, 0.3, 0.15, 0.1, 0, 1),
 }
 
-REPORT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out",
-                      "parity_report.jsonl")
+REPORT = os.environ.get("PARITY_REPORT") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "parity_report.jsonl")
 
 
 def report(**kw):
@@ -255,6 +255,10 @@ def test_ials_reg_exp0_trajectory_matches_oracle(tmp_path, ml1m_csr, dim):
                     str(out), str(reg), str(w), str(alpha), str(bw), str(eta), str(epan),
                     str(snr), "0.5"],
                    check=True, capture_output=True, timeout=300, env=env)
+    if os.environ.get("PARITY_DUMP_DIR"):  # the GPU trajectory for scripts/traj_f64.py
+        import shutil
+        shutil.copy(str(out), os.path.join(os.environ["PARITY_DUMP_DIR"],
+                                           f"ials_reg_exp0_d{dim}.bin"))
     U, V, loss, dw, xi, mw, _ = _read_dump(str(out), epochs, False)
     nu, ni, up, uc, ip, ic = ml1m_csr
     m = O.Model(oid, dim, nu, ni, reg=reg, w=w, alpha=alpha, reg_exp=0.0, seed=1)

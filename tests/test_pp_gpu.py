@@ -235,3 +235,45 @@ def test_pp_sharded_bitwise(quirk_data, world, dim, bs, kind):
                                   ref.get_embeddings(fh.SIDE_USER))
     for c in ctxs + [ref]:
         c.close()
+
+
+def test_pp_sync_pending_rejected(quirk_data):
+    """External-exchange mode: a sharded block step leaves a snapshot for
+    frecsys_pp_sync; another pp_step or pp_predict before the sync is refused
+    (FRECSYS_ERR_INVALID, 'pp_sync pending'), and the sequence goes on after
+    the sync."""
+    from test_sharded_gpu import _allgather_rows, _allreduce_gram
+    nu, ni, up, uc, ip, ic = quirk_data
+    urix, irix = _rix(uc)
+    ctxs = []
+    for r in range(2):
+        c = fh.Context(32, nu, ni, device=0)
+        c.comm_init(2, r, None)
+        c.load_csr(fh.SIDE_USER, up, uc)
+        c.load_csr(fh.SIDE_ITEM, ip, ic)
+        c.init_embeddings(1, 0.1)
+        c.pp_set_rating_index(fh.SIDE_USER, urix)
+        c.pp_set_rating_index(fh.SIDE_ITEM, irix)
+        c.pp_predict(fh.SIDE_USER)
+        ctxs.append(c)
+    _allreduce_gram(ctxs, fh.SIDE_ITEM)
+    for c in ctxs:
+        c.pp_step(fh.SIDE_USER, 0, 16, 0.003, 0.1)
+    for c in ctxs:
+        with pytest.raises(fh.FrecsysError, match="pp_sync pending"):
+            c.pp_step(fh.SIDE_USER, 16, 32, 0.003, 0.1)
+        with pytest.raises(fh.FrecsysError, match="pp_sync pending"):
+            c.pp_step(fh.SIDE_ITEM, 0, 16, 0.003, 0.1)
+        with pytest.raises(fh.FrecsysError, match="pp_sync pending"):
+            c.pp_predict(fh.SIDE_USER)
+    _allgather_rows(ctxs, fh.SIDE_USER)
+    for c in ctxs:
+        c.pp_sync(fh.SIDE_USER)
+        with pytest.raises(fh.FrecsysError, match="no sharded block step"):
+            c.pp_sync(fh.SIDE_USER)
+    for c in ctxs:
+        c.pp_step(fh.SIDE_USER, 16, 32, 0.003, 0.1)
+    _allgather_rows(ctxs, fh.SIDE_USER)
+    for c in ctxs:
+        c.pp_sync(fh.SIDE_USER)
+        c.close()
