@@ -147,6 +147,14 @@ struct frecsys_ctx {
   // (wide_syrk.hip; FRECSYS_WIDE_PRESPLIT=0: the register-staged SYRK)
   char* wide_xs = nullptr;
   size_t cap_wide_xs = 0;
+  // the history-space wide bucket (dual.hip, 256 < h_eff <= 512): split Z
+  // fragments, Cholesky slots of S, z
+  char* dw_zs = nullptr;
+  size_t cap_dw_zs = 0;
+  float* dw_slots = nullptr;
+  size_t cap_dw_slots = 0;
+  float* dw_z = nullptr;
+  size_t cap_dw_z = 0;
   bool wide_presplit = true;
   // FRECSYS_WIDE_WS_MB: the budget of EACH of the two wide d-space buffers
   // (the batch workspace of A tiles, and the long-history slabs): up to
@@ -977,9 +985,11 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   if (const char* v = getenv("FRECSYS_CHOL_BASIS")) c->chol_basis_on = atoi(v);
   // d-space / history-space crossover: by flops h = d, but at Dp <= 256 the
   // d-space kernel overtakes the TH = 8 bucket (225 < h <= 256) in time (epoch
-  // 15.6 -> 15.1 ms at the ML-20M shape, threshold sweep in DESIGN.md 3.2); at
-  // Dp = 512 / 1024 the d-space Cholesky is 8x / 64x dearer: keep 256.
-  c->dual_max_h = Dp <= 256 ? 224 : 256;
+  // 15.6 -> 15.1 ms at the ML-20M shape, threshold sweep in DESIGN.md 3.2).
+  // Dp = 1024: the wide bucket (256 < h_eff <= 512, dual.hip) as well (config
+  // 5 epoch 1470 -> 1274 ms); Dp = 512: 256 (the wide bucket at 384 / 512
+  // measured 124 / 129 ms against 115 at MSD).
+  c->dual_max_h = Dp <= 256 ? 224 : Dp == 1024 ? 512 : 256;
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H")) c->dual_max_h = atoi(v);
   if (const char* v = getenv("FRECSYS_DUAL_SERIAL")) c->dual_serial = atoi(v);
   if (const char* v = getenv("FRECSYS_SPLIT_ROWS")) c->split_rows = atoi(v);
@@ -996,12 +1006,14 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   }
   if (const char* v = getenv("FRECSYS_WIDE_WS_MB")) c->wide_ws_mb = std::max(1, atoi(v));
   if (const char* v = getenv("FRECSYS_WIDE_PRESPLIT")) c->wide_presplit = atoi(v) != 0;
-  c->dual_max_h = std::min(c->dual_max_h, 32 * kDualMaxTiles);
+  // the wide dims add the wide bucket (256 < h_eff <= 512, dual.hip)
+  const int max_h_cap = Dp >= 512 ? kDualWideMaxH : 32 * kDualMaxTiles;
+  c->dual_max_h = std::min(c->dual_max_h, max_h_cap);
   for (int t = 0; t < 3; ++t) c->dual_max_h_side[t] = c->dual_max_h;
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H_USER"))
-    c->dual_max_h_side[0] = std::min(atoi(v), 32 * kDualMaxTiles);
+    c->dual_max_h_side[0] = std::min(atoi(v), max_h_cap);
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H_ITEM"))
-    c->dual_max_h_side[1] = std::min(atoi(v), 32 * kDualMaxTiles);
+    c->dual_max_h_side[1] = std::min(atoi(v), max_h_cap);
   for (int s = 0; s < 2; ++s) {
     const size_t rows = (size_t)std::max<int64_t>(c->n[s], 1);
     if (hipMalloc((void**)&c->emb[s], sizeof(float) * rows * Dp) != hipSuccess ||
@@ -1064,6 +1076,9 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
   if (c->chol_work) (void)hipFree(c->chol_work);
   if (c->wide_ws) (void)hipFree(c->wide_ws);
   if (c->wide_xs) (void)hipFree(c->wide_xs);
+  if (c->dw_zs) (void)hipFree(c->dw_zs);
+  if (c->dw_slots) (void)hipFree(c->dw_slots);
+  if (c->dw_z) (void)hipFree(c->dw_z);
   if (c->d_scores) (void)hipFree(c->d_scores);
   if (c->d_rows) (void)hipFree(c->d_rows);
   for (int s = 0; s < 2; ++s) {
@@ -1725,6 +1740,29 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
         HIP_TRY(c, hipStreamWaitEvent(c->stream3, c->ev_fork3, 0));
       }
       int64_t lo = n_dspace;
+      if (c->dual_max_h_side[side] > 32 * kDualMaxTiles && lo < n_nonempty) {
+        // the wide bucket, 256 < h_eff <= 512, in batches of its workspace
+        const int64_t hi = std::min(n_nonempty, first_le(32 * kDualMaxTiles));
+        const size_t per = dual_wide_zs_bytes(c->Dp) + sizeof(float) * (dual_wide_slot_floats() + 512);
+        const int64_t nbat = std::max<int64_t>(
+            1, std::min<int64_t>(hi - lo, (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / per)));
+        if (hi > lo) {
+          rc = ensure(c, &c->dw_zs, &c->cap_dw_zs, dual_wide_zs_bytes(c->Dp) * (size_t)nbat);
+          if (rc) return rc;
+          rc = ensure(c, &c->dw_slots, &c->cap_dw_slots, dual_wide_slot_floats() * (size_t)nbat);
+          if (rc) return rc;
+          rc = ensure(c, &c->dw_z, &c->cap_dw_z, (size_t)512 * nbat);
+          if (rc) return rc;
+        }
+        for (int64_t b0 = lo; b0 < hi; b0 += nbat) {
+          d.order = a.order + b0;
+          d.n_rows = std::min(nbat, hi - b0);
+          d.pos0 = b0 - n_dspace;
+          d.prof = nullptr;
+          HIP_TRY(c, launch_dual_wide(d, c->dw_zs, c->dw_slots, c->dw_z, a.fail, c->stream));
+        }
+        lo = std::max(lo, hi);
+      }
       for (int tiles = kDualMaxTiles; tiles >= 1 && lo < n_nonempty; --tiles) {
         const int64_t hi = std::min(n_nonempty, first_le(32 * (tiles - 1)));
         if (hi > lo) {

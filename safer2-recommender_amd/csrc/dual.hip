@@ -819,6 +819,214 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   if (lane == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
+
+// ---------------------------------------------------------------------
+// Wide bucket: 256 < h_eff <= 512 at Dp = 512 / 1024.  S (up to 512 x 512)
+// no longer fits a CU's LDS, so the bucket runs the same algebra as
+// dual_solve_kernel through HBM workspaces, a batch of entities at a time:
+//   dual_wide_z_kernel    one workgroup (512 threads, thread j = row j) per
+//                         entity: the recurrence z_j[k] = y_j[k] - l_k
+//                         z_j[k-1] scaled by c_j D_k^-1/2, written as the
+//                         3-piece bf16 split fragments of the MFMA operand
+//                         (zs: [Dp/16][piece][k-half][512] x bf16x8), and
+//                         s (c_j for real rows) as the rhs of the slot;
+//   dual_wide_s_kernel    S = I + Z D^-1 Z^T on the bf16 matrix cores
+//                         (mfma_x6, fp32-accurate) straight from those
+//                         fragments: a workgroup per (entity, 128 x 128
+//                         block pair), each wave a 64 x 64 quarter (2 x 2
+//                         tiles, fragments shared), into the Cholesky slot
+//                         (row-major 32 x 32 tiles, tidx order);
+//   wide_chol_kernel<16>  (wide.hip) z = S^-1 s;
+//   dual_wide_v_kernel    Y^T (c.*z) into out_rot, as dual_solve_kernel's
+//                         epilogue, for dual_sweep_kernel + the back rotation.
+// Padding rows (j >= h_eff) have c_j = 0: zero fragments, identity rows of S,
+// s_j = 0, so z_j = 0.
+// ---------------------------------------------------------------------
+constexpr int kWideHP = 512;
+
+__device__ __forceinline__ int64_t wz_gran(int kb, int p, int hh, int j) {
+  return (((int64_t)kb * 3 + p) * 2 + hh) * kWideHP + j;
+}
+
+__global__ void __launch_bounds__(512) dual_wide_z_kernel(DualArgs a, bf16x8* zs_all,
+                                                          float* slots, int64_t slot_floats) {
+  __shared__ float lsub[kMaxDp], dsq[kMaxDp];
+  const int tid = threadIdx.x, Dp = a.Dp;
+  const QueueRec rec = a.order[blockIdx.x];
+  const int64_t e = rec.entity, h = rec.h, p0 = rec.p0;
+  const bool vk = is_v_kind(a.kind), uk = is_u_kind(a.kind);
+  int64_t extra = 0;
+  if (vk && a.quirk && h > 128 && (h % 128) != 0) extra = 128 - (h % 128);
+  const int ntot = (int)(h + extra);  // <= kWideHP (host bucketing)
+  float mu, lam, omega;
+  dual_scalars(a, e, h, mu, lam, omega);
+  int id = 0;
+  float cj = 0.0f;
+  if (tid < ntot) {
+    id = a.col[p0 + virt_pos_d(tid, h)];
+    cj = vk ? sqrtf(a.other_weight[id]) : (uk ? sqrtf(omega / (float)h) : 1.0f);
+  }
+  float* slot = slots + (int64_t)blockIdx.x * slot_floats;
+  slot[slot_floats - kWideHP + tid] = tid < h ? cj : 0.0f;  // s, the rhs of S z = s
+  const int64_t pp = a.pos0 + blockIdx.x;
+  for (int k = tid; k < Dp; k += 512) {
+    lsub[k] = a.table[blk_t(pp, 0, k, Dp)];
+    dsq[k] = a.table[blk_t(pp, 1, k, Dp)];
+  }
+  __syncthreads();
+  bf16x8* zs = zs_all + (int64_t)blockIdx.x * (Dp / 16) * 3 * 2 * kWideHP;
+  const float* row = a.Xrot + (int64_t)id * Dp;
+  float4 y[4], yn[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) y[q] = *reinterpret_cast<const float4*>(row + 4 * q);
+  float z = 0.0f;
+#pragma unroll 1
+  for (int kb = 0; kb < Dp / 16; ++kb) {
+    if (kb + 1 < Dp / 16) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) yn[q] = *reinterpret_cast<const float4*>(row + 16 * (kb + 1) + 4 * q);
+    }
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float4 y4 = y[2 * hh + (u >> 2)];
+        const float yv = (u & 3) == 0 ? y4.x : (u & 3) == 1 ? y4.y : (u & 3) == 2 ? y4.z : y4.w;
+        const int k = 16 * kb + 8 * hh + u;
+        z = yv - lsub[k] * z;
+        v[u] = (cj * z) * dsq[k];
+      }
+      bf16x8 f[3];
+      split3x8(v, f);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) zs[wz_gran(kb, p, hh, tid)] = f[p];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[q] = yn[q];
+  }
+}
+
+// grid: (entity of the batch) x 10 block pairs (BI >= BJ of 4 x 4 blocks of
+// 128); 256 threads, wave w: tiles rows 4 BI + 2 (w >> 1) + {0, 1}, columns
+// 4 BJ + 2 (w & 1) + {0, 1} (upper tiles of a diagonal pair skipped).
+__global__ void __launch_bounds__(256) dual_wide_s_kernel(const bf16x8* zs_all, int Dp,
+                                                          const QueueRec* order, int quirk_v,
+                                                          float* slots, int64_t slot_floats) {
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t b = blockIdx.x / 10;
+  int pr = blockIdx.x % 10, BI = 0;
+  while ((BI + 1) * (BI + 2) / 2 <= pr) ++BI;
+  const int BJ = pr - BI * (BI + 1) / 2;
+  const int I0 = 4 * BI + 2 * (wave >> 1), J0 = 4 * BJ + 2 * (wave & 1);
+  float* slot = slots + b * slot_floats;
+  // tiles past the entity's rows: S = I there, no products
+  const QueueRec rec = order[b];
+  int64_t extra = 0;
+  if (quirk_v && rec.h > 128 && (rec.h % 128) != 0) extra = 128 - (rec.h % 128);
+  const int te = (int)((rec.h + extra + 31) / 32);  // tiles holding rows
+  const bf16x8* zs = zs_all + b * (Dp / 16) * 3 * 2 * kWideHP;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) acc[u][v] = f32x16{0.f};
+  const bool live = I0 < te && J0 < te && !(BI == BJ && J0 > I0 + 1);
+  if (live) {
+    bf16x8 fa[2][3], fb[2][3];
+    auto load = [&](int kb, bf16x8(&A)[2][3], bf16x8(&B)[2][3]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          A[u][p] = zs[wz_gran(kb, p, hi, 32 * (I0 + u) + lo)];
+          B[u][p] = zs[wz_gran(kb, p, hi, 32 * (J0 + u) + lo)];
+        }
+    };
+    load(0, fa, fb);
+#pragma unroll 1
+    for (int kb = 0; kb < Dp / 16; ++kb) {
+      bf16x8 na[2][3], nb[2][3];
+      if (kb + 1 < Dp / 16) load(kb + 1, na, nb);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          if (!(BI == BJ && J0 + v > I0 + u)) acc[u][v] = mfma_x6(fa[u], fb[v], acc[u][v]);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          fa[u][p] = na[u][p];
+          fb[u][p] = nb[u][p];
+        }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int I = I0 + u, J = J0 + v;
+      if (J > I) continue;
+      float* tile = slot + (int64_t)tidx(I, J) * 1024;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int r = acc_row(q, hi);
+        tile[r * 32 + lo] = acc[u][v][q] + ((I == J && r == lo) ? 1.0f : 0.0f);
+      }
+    }
+}
+
+// v = Y^T (c.*z) of one entity (z: the Cholesky output row of its slot)
+__global__ void __launch_bounds__(256) dual_wide_v_kernel(DualArgs a, const float* zb) {
+  __shared__ float red[1024];
+  const int tid = threadIdx.x, Dp = a.Dp;
+  const QueueRec rec = a.order[blockIdx.x];
+  const int64_t e = rec.entity, h = rec.h, p0 = rec.p0;
+  const bool vk = is_v_kind(a.kind), uk = is_u_kind(a.kind);
+  int64_t extra = 0;
+  if (vk && a.quirk && h > 128 && (h % 128) != 0) extra = 128 - (h % 128);
+  const int ntot = (int)(h + extra);
+  float mu, lam, omega;
+  dual_scalars(a, e, h, mu, lam, omega);
+  const float cu = uk ? sqrtf(omega / (float)h) : 1.0f;
+  const float* z = zb + (int64_t)blockIdx.x * kWideHP;
+  const int D4 = Dp >> 2, R = 256 / D4;
+  const int c4 = tid % D4, g = tid / D4;
+  float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j0 = g; j0 < ntot; j0 += 8 * R) {
+    float4 rv[8];
+    float wv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + u * R;
+      rv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      wv[u] = 0.0f;
+      if (j < ntot) {
+        const int id = a.col[p0 + virt_pos_d(j, h)];
+        const float cj = vk ? sqrtf(a.other_weight[id]) : cu;
+        wv[u] = cj * z[j];
+        rv[u] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)id * Dp + 4 * c4);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      acc4.x += wv[u] * rv[u].x;
+      acc4.y += wv[u] * rv[u].y;
+      acc4.z += wv[u] * rv[u].z;
+      acc4.w += wv[u] * rv[u].w;
+    }
+  }
+  *reinterpret_cast<float4*>(red + g * Dp + 4 * c4) = acc4;
+  __syncthreads();
+  for (int i = tid; i < Dp; i += 256) {
+    float v = 0.0f;
+    for (int gg = 0; gg < R; ++gg) v += red[gg * Dp + i];
+    a.out_rot[blk_v(a.pos0 + blockIdx.x, i, Dp)] = v;
+  }
+}
+
 template <int TH, bool BF>
 hipError_t launch_wave_v(const DualArgs& a, hipStream_t s) {
   using C = WaveCfg<TH, BF>;
@@ -860,6 +1068,26 @@ hipError_t launch_dual_ldl(const DualArgs& a, hipStream_t s) {
   if (a.Dp < 64 || a.Dp > kMaxDp || (a.Dp & 31)) return hipErrorInvalidValue;
   const unsigned nb = (unsigned)((a.n_rows + 255) / 256);
   hipLaunchKernelGGL(dual_ldl_kernel, dim3(nb), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+size_t dual_wide_zs_bytes(int Dp) { return (size_t)(Dp / 16) * 3 * 2 * kWideHP * sizeof(bf16x8); }
+size_t dual_wide_slot_floats() { return (size_t)16 * 17 / 2 * 1024 + kWideHP; }
+
+hipError_t launch_dual_wide(const DualArgs& a, void* zs, float* slots, float* zbuf,
+                            unsigned long long* fail, hipStream_t s) {
+  if (a.n_rows <= 0) return hipSuccess;
+  if (a.Dp != 512 && a.Dp != 1024) return hipErrorInvalidValue;
+  const int64_t sf = (int64_t)dual_wide_slot_floats();
+  bf16x8* z = reinterpret_cast<bf16x8*>(zs);
+  hipLaunchKernelGGL(dual_wide_z_kernel, dim3((unsigned)a.n_rows), dim3(512), 0, s, a, z, slots, sf);
+  hipLaunchKernelGGL(dual_wide_s_kernel, dim3((unsigned)(a.n_rows * 10)), dim3(256), 0, s,
+                     (const bf16x8*)z, a.Dp, a.order,
+                     (int)(is_v_kind(a.kind) && a.quirk), slots, sf);
+  hipError_t e = launch_wide_chol_slots(a.order, a.n_rows, slots, zbuf, fail, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(dual_wide_v_kernel, dim3((unsigned)a.n_rows), dim3(256), 0, s, a,
+                     (const float*)zbuf);
   return hipGetLastError();
 }
 

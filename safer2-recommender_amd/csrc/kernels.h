@@ -174,6 +174,20 @@ hipError_t launch_dual_sweep(const DualArgs& a, hipStream_t s);
 // One launch per history bucket: every entity of a.order has
 // 32*(tiles-1) < h_eff <= 32*tiles.
 hipError_t launch_dual(int tiles, const DualArgs& a, hipStream_t s);
+// The wide bucket (dual.hip): 256 < h_eff <= 512 at Dp = 512 / 1024, the
+// entities a.order[0..n_rows) (positions a.pos0..) through HBM workspaces:
+// zs (dual_wide_zs_bytes per entity), slots (dual_wide_slot_floats per
+// entity), zbuf (512 floats per entity); Cholesky failures into fail.
+constexpr int kDualWideMaxH = 512;
+size_t dual_wide_zs_bytes(int Dp);
+size_t dual_wide_slot_floats();
+hipError_t launch_dual_wide(const DualArgs& a, void* zs, float* slots, float* zbuf,
+                            unsigned long long* fail, hipStream_t s);
+// wide_chol_kernel<16> over n Cholesky slots (row-major 32 x 32 tiles of a
+// 512 x 512 SPD matrix + its rhs): solution of slot i into out[512 i ..),
+// a failure reported as order[i].entity.
+hipError_t launch_wide_chol_slots(const QueueRec* order, int64_t n, float* slots, float* out,
+                                  unsigned long long* fail, hipStream_t s);
 // Householder tridiagonalisation G = Q T Q^T of a Dp x Dp symmetric matrix
 // (one workgroup): T's diagonal / subdiagonal, the reflectors (row k of Vh,
 // entries k+1..Dp-1) and their tau.  With Q (only when tridiag_forms_q(Dp)):

@@ -675,10 +675,9 @@ __global__ void __launch_bounds__(256)
 // contraction, the compiler pairs some of these products into v_pk_mul_f32
 // (rounded, then added) differently in each kernel, and the two kernels'
 // y differed in the last bit in about one element in 500 ----
-template <int T>
+template <int T, int NW = 8>
 __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, float* xv,
                                                 float* part, int wave, int lo, int hi) {
-  constexpr int NW = 8;
   auto gtile = [&](int I, int J) { return slot + (int64_t)tidx(I, J) * 1024; };
 #pragma unroll 1
   for (int p = T - 1; p >= 0; --p) {
@@ -737,7 +736,7 @@ __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, fl
 template <int T>
 __global__ void __launch_bounds__(512)
     __attribute__((amdgpu_waves_per_eu(T == 16 ? kWideCholWPE : 2, 8)))
-    wide_chol_kernel(SolveArgs a, int64_t pos0, float* ws) {
+    wide_chol_kernel(SolveArgs a, int64_t pos0, float* ws, int slot_out) {
   constexpr int Dp = 32 * T, NT = T * (T + 1) / 2, NW = 8;
   typedef float f32x4v __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -766,7 +765,14 @@ __global__ void __launch_bounds__(512)
 
   // C_I = (A_Ip - sum_{q<p} L_Iq L_pq^T)^T in accumulator registers: A_Ip^T
   // as its rows, L_Iq streamed from the workspace into operand registers
-  // (k = 16 hi + s), the next tile's loads in flight under each product
+  // (k = 16 hi + s), a ring of PF tiles: the loads of tiles q+1 .. q+PF-1
+  // in flight under the product of tile q (the loop unrolled by PF so that
+  // every ring slot is a fixed set of registers)
+  constexpr int PF = T == 16 ? 2 : 4;
+  // T = 32: split-bf16 products (common.h mfma_x6, fp32-accurate) with the
+  // operands split in registers; T = 16 keeps f32 MFMA (at 128 registers the
+  // splits spill, and its time was unchanged)
+  constexpr bool X6 = T == 32;
   auto panel_sum = [&](int I, int p) __attribute__((always_inline)) {
     const float* Aip = gtile(I, p) + lo * 32 + 4 * hi;
     f32x16 c;
@@ -776,24 +782,52 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
       for (int j = 0; j < 4; ++j) c[4 * g + j] = v[j];
     }
-    f32x4v cur[4], nxt[4];
-    if (p > 0) {
-      const f32x4v* L0 = reinterpret_cast<const f32x4v*>(gtile(I, 0) + lo * 32 + 16 * hi);
+    f32x4v ring[PF][4];
+    auto ld = [&](int q, f32x4v(&dst)[4]) __attribute__((always_inline)) {
+      if constexpr (X6) {  // k = 16 g + 8 hi + t of row lo (the bf16 MFMA operand layout)
+        const float* L = gtile(I, q) + lo * 32 + 8 * hi;
+        dst[0] = *reinterpret_cast<const f32x4v*>(L);
+        dst[1] = *reinterpret_cast<const f32x4v*>(L + 4);
+        dst[2] = *reinterpret_cast<const f32x4v*>(L + 16);
+        dst[3] = *reinterpret_cast<const f32x4v*>(L + 20);
+      } else {  // k = 16 hi + s
+        const f32x4v* L = reinterpret_cast<const f32x4v*>(gtile(I, q) + lo * 32 + 16 * hi);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = L0[j];
-    }
-#pragma unroll 1
-    for (int q = 0; q < p; ++q) {
-      if (q + 1 < p) {
-        const f32x4v* Ln = reinterpret_cast<const f32x4v*>(gtile(I, q + 1) + lo * 32 + 16 * hi);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) nxt[j] = Ln[j];
+        for (int j = 0; j < 4; ++j) dst[j] = L[j];
       }
-      const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+    };
 #pragma unroll
-      for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], cur[s2 >> 2][s2 & 3], c);
+    for (int j = 0; j < PF - 1; ++j)
+      if (j < p) ld(j, ring[j]);
+#pragma unroll 1
+    for (int q0 = 0; q0 < p; q0 += PF) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) cur[j] = nxt[j];
+      for (int j = 0; j < PF; ++j) {
+        const int q = q0 + j;
+        if (q < p) {
+          if (q + PF - 1 < p) ld(q + PF - 1, ring[(j + PF - 1) % PF]);
+          if constexpr (X6) {
+            const float* P = rowL + q * LP + lo * 33 + 8 * hi;
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+              float pv[8], lv[8];
+#pragma unroll
+              for (int t = 0; t < 8; ++t) {
+                pv[t] = -P[16 * g + t];
+                lv[t] = ring[j][2 * g + (t >> 2)][t & 3];
+              }
+              bf16x8 pf[3], lf[3];
+              split3x8(pv, pf);
+              split3x8(lv, lf);
+              c = mfma_x6(pf, lf, c);
+            }
+          } else {
+            const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) c = mfma32(-P[s2], ring[j][s2 >> 2][s2 & 3], c);
+          }
+        }
+      }
     }
     return c;
   };
@@ -841,10 +875,27 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
       for (int q = 0; q < 16; ++q) d[q] = App[acc_row(q, hi) * 32 + lo];
 #pragma unroll 1
-      for (int q = 0; q < p; ++q) {  // d -= L_pq L_pq^T (k = 16 hi + s)
-        const float* P = rowL + q * LP + lo * 33 + 16 * hi;
+      for (int q = 0; q < p; ++q) {  // d -= L_pq L_pq^T
+        if constexpr (X6) {
+          const float* P = rowL + q * LP + lo * 33 + 8 * hi;  // k = 16 g + 8 hi + t
 #pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
+          for (int g = 0; g < 2; ++g) {
+            float pv[8], nv[8];
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              pv[t] = P[16 * g + t];
+              nv[t] = -pv[t];
+            }
+            bf16x8 pf[3], nf[3];
+            split3x8(pv, pf);
+            split3x8(nv, nf);
+            d = mfma_x6(nf, pf, d);
+          }
+        } else {
+          const float* P = rowL + q * LP + lo * 33 + 16 * hi;  // k = 16 hi + s
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2) d = mfma32(-P[s2], P[s2], d);
+        }
       }
       // opaque copies of the lane coordinates: the 48 swizzled / padded
       // addresses below are formed here with a few VALU ops each, not hoisted
@@ -905,7 +956,10 @@ __global__ void __launch_bounds__(512)
     __syncthreads();
   }
   wide_back_subst<T>(slot, yv, xv, part, wave, lo, hi);
-  for (int i = tid; i < Dp; i += 512) a.out[e * Dp + i] = xv[i];
+  // slot_out: the solution of slot b into out[Dp b ..) (the history-space
+  // wide bucket's S systems), else into the entity's row
+  const int64_t orow = slot_out ? (int64_t)blockIdx.x : e;
+  for (int i = tid; i < Dp; i += 512) a.out[orow * Dp + i] = xv[i];
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
@@ -1458,6 +1512,7 @@ size_t wide_chol_lds_bytes(int Dp) {
 }
 
 
+
 }  // namespace
 
 bool wide_dim(int Dp) { return Dp == 512 || Dp == 1024; }
@@ -1498,6 +1553,26 @@ hipError_t launch_wide_gram_final(int Dp, const float* gslabs, int64_t ngroup, f
                                   hipStream_t s) {
   hipLaunchKernelGGL(wide_gram_reduce_kernel, dim3((unsigned)(((int64_t)Dp * Dp + 255) / 256)),
                      dim3(256), 0, s, gslabs, ngroup, G, Dp);
+  return hipGetLastError();
+}
+
+hipError_t launch_wide_chol_slots(const QueueRec* order, int64_t n, float* slots, float* out,
+                                  unsigned long long* fail, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel<16>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)wide_chol_lds_bytes(512));
+    if (err != hipSuccess) return err;
+    attr = true;
+  }
+  SolveArgs a{};
+  a.order = order;
+  a.out = out;
+  a.fail = fail;
+  hipLaunchKernelGGL(wide_chol_kernel<16>, dim3((unsigned)n), dim3(512), wide_chol_lds_bytes(512),
+                     s, a, (int64_t)0, slots, 1);
   return hipGetLastError();
 }
 
@@ -1558,10 +1633,10 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
     else if (Dp == 512)
       hipLaunchKernelGGL(wide_chol_kernel<16>, dim3((unsigned)nb), dim3(512),
-                         wide_chol_lds_bytes(Dp), s, a, s0, ws);
+                         wide_chol_lds_bytes(Dp), s, a, s0, ws, 0);
     else
       hipLaunchKernelGGL(wide_chol_kernel<32>, dim3((unsigned)nb), dim3(512),
-                         wide_chol_lds_bytes(Dp), s, a, s0, ws);
+                         wide_chol_lds_bytes(Dp), s, a, s0, ws, 0);
   }
   return hipGetLastError();
 }

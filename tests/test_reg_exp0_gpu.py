@@ -57,13 +57,14 @@ def test_reg_exp0_well_conditioned_half_step(monkeypatch, ml1m_csr, dim, side): 
         assert ctx.work("basis_chol")[2] == (basis == "chol")
         assert ctx.counter("hspace_reruns") == 0
         outs[basis] = ctx.get_embeddings(s)
+        max_h = ctx.history_space_max_h()  # 256; 512 at Dp = 1024 (the wide bucket)
         X = U if side == "user" else V
         ctx.close()
     G0 = O.gramian(X0)
     Xo, rc = O.step(ptr, col, X0, G0, 0, REG, W, reg_exp=0.0, out=X.copy())
     assert rc == 0
     h = np.diff(ptr)
-    short, long_ = (h > 0) & (h <= 256), h > 256
+    short, long_ = (h > 0) & (h <= max_h), h > max_h
     errs = {b: rel_rows(x, Xo) for b, x in outs.items()}
     # float64 solutions of the worst rows of either basis and of the oracle's
     # own error there (lambda = reg for every row)
