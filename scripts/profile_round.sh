@@ -10,6 +10,7 @@
 #      bracketed FETCH / WRITE passes) and the FETCH_SIZE width calibration,
 #      merged into latest_pmc.json (halfstep_item)
 # Usage: profile_round.sh <outdir under gpurun_out> [workloads...]
+#   SKIP_BENCH=1: no step 1; SKIP_TAIL=1: no steps 3-4 (to split the pass over calls)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
@@ -18,8 +19,10 @@ OUT=gpurun_out/$NAME
 shift
 WL=${*:-ials_ml20m_d256 safer2_ml20m_d256 ials_msd_d512}
 mkdir -p $OUT
-timeout -k 10 420 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; exit 1; }
-echo "bench ok"
+if [ -z "$SKIP_BENCH" ]; then
+  timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; exit 1; }
+  echo "bench ok"
+fi
 for w in $WL; do
   ARGS="--workload $w --extras= --steps 10 --warmup 1 --cpu-seconds 0 --quiet"
   timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/trace_$w -o run --output-format csv -- python3 bench.py $ARGS > $OUT/trace_$w.log 2>&1 || { echo trace $w failed; exit 2; }
@@ -29,6 +32,7 @@ for w in $WL; do
   python3 scripts/pmc_summary.py $w $(ls $OUT/fetch_$w/*counter_collection.csv $OUT/fetch_$w/*/*counter_collection.csv 2>/dev/null | head -1) $(ls $OUT/write_$w/*counter_collection.csv $OUT/write_$w/*/*counter_collection.csv 2>/dev/null | head -1) 2 $OUT/pmc_$w.json $OUT/latest_pmc.json > $OUT/pmc_$w.txt || { echo summary $w failed; exit 5; }
   echo "$w ok"
 done
+[ -n "$SKIP_TAIL" ] && { echo done; exit 0; }
 SARGS="--workload ials_ml20m_d256 --extras= --steps 2 --warmup 1 --cpu-seconds 0 --quiet --allow-env"
 FRECSYS_DUAL_SERIAL=1 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/trace_serial -o run --output-format csv -- python3 bench.py $SARGS > $OUT/trace_serial.log 2>&1 || { echo serial trace failed; exit 6; }
 FRECSYS_DUAL_SERIAL=1 timeout -s KILL 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/sq_serial -o run --output-format csv -- python3 bench.py $SARGS > $OUT/sq_serial.log 2>&1 || { echo sq pass failed; exit 7; }
