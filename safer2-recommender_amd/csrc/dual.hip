@@ -875,6 +875,8 @@ __global__ void __launch_bounds__(512) dual_wide_z_kernel(DualArgs a, bf16x8* zs
   }
   __syncthreads();
   bf16x8* zs = zs_all + (int64_t)blockIdx.x * (Dp / 16) * 3 * 2 * kWideHP;
+  // rows past the entity's last tile are never read (dual_wide_s_kernel)
+  if (tid >= 32 * ((ntot + 31) / 32)) return;
   const float* row = a.Xrot + (int64_t)id * Dp;
   float4 y[4], yn[4];
 #pragma unroll
@@ -1084,7 +1086,8 @@ hipError_t launch_dual_wide(const DualArgs& a, void* zs, float* slots, float* zb
   hipLaunchKernelGGL(dual_wide_s_kernel, dim3((unsigned)(a.n_rows * 10)), dim3(256), 0, s,
                      (const bf16x8*)z, a.Dp, a.order,
                      (int)(is_v_kind(a.kind) && a.quirk), slots, sf);
-  hipError_t e = launch_wide_chol_slots(a.order, a.n_rows, slots, zbuf, fail, s);
+  hipError_t e = launch_wide_chol_slots(a.order, a.n_rows, slots, zbuf, fail,
+                                        (int)(is_v_kind(a.kind) && a.quirk), s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(dual_wide_v_kernel, dim3((unsigned)a.n_rows), dim3(256), 0, s, a,
                      (const float*)zbuf);

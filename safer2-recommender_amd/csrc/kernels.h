@@ -185,9 +185,10 @@ hipError_t launch_dual_wide(const DualArgs& a, void* zs, float* slots, float* zb
                             unsigned long long* fail, hipStream_t s);
 // wide_chol_kernel<16> over n Cholesky slots (row-major 32 x 32 tiles of a
 // 512 x 512 SPD matrix + its rhs): solution of slot i into out[512 i ..),
-// a failure reported as order[i].entity.
+// a failure reported as order[i].entity; only the tiles holding the
+// h_eff = order[i].h (+ the tail quirk's rows when quirk_v) rows are factored.
 hipError_t launch_wide_chol_slots(const QueueRec* order, int64_t n, float* slots, float* out,
-                                  unsigned long long* fail, hipStream_t s);
+                                  unsigned long long* fail, int quirk_v, hipStream_t s);
 // Householder tridiagonalisation G = Q T Q^T of a Dp x Dp symmetric matrix
 // (one workgroup): T's diagonal / subdiagonal, the reflectors (row k of Vh,
 // entries k+1..Dp-1) and their tau.  With Q (only when tridiag_forms_q(Dp)):

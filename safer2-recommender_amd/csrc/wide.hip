@@ -677,10 +677,11 @@ __global__ void __launch_bounds__(256)
 // y differed in the last bit in about one element in 500 ----
 template <int T, int NW = 8>
 __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, float* xv,
-                                                float* part, int wave, int lo, int hi) {
+                                                float* part, int wave, int lo, int hi,
+                                                int te = T) {
   auto gtile = [&](int I, int J) { return slot + (int64_t)tidx(I, J) * 1024; };
 #pragma unroll 1
-  for (int p = T - 1; p >= 0; --p) {
+  for (int p = te - 1; p >= 0; --p) {
     // every workspace load of the step is issued before the first use (the
     // x-independent L values: one HBM round trip per step instead of one per
     // four values); the summation orders are unchanged
@@ -691,7 +692,7 @@ __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, fl
       for (int i = 0; i < 32; ++i) li[i] = Li[i * 32 + lo];
     }
     float pr = 0.0f;
-    for (int q = p + 1 + wave; q < T; q += NW) {
+    for (int q = p + 1 + wave; q < te; q += NW) {
       const float* L = gtile(q, p) + 16 * hi * 32 + lo;
       float lv[16];
 #pragma unroll
@@ -757,6 +758,15 @@ __global__ void __launch_bounds__(512)
   const QueueRec rec = a.order[pos0 + blockIdx.x];
   const int64_t e = rec.entity;
   if (rec.h == 0) return;
+  // slot_out (the history-space wide bucket's S): only the tiles holding
+  // the h_eff rows are factored -- the padding is the identity with a zero
+  // rhs, so its solution is 0 (2: ProjectV with the tail quirk's rows)
+  int te = T;
+  if (slot_out) {
+    int64_t heff = rec.h;
+    if (slot_out == 2 && heff > 128 && (heff % 128) != 0) heff += 128 - (heff % 128);
+    te = (int)min<int64_t>(T, (heff + 31) / 32);
+  }
   float* slot = ws + (int64_t)blockIdx.x * ((int64_t)NT * 1024 + Dp);
   auto gtile = [&](int I, int J) { return slot + (int64_t)tidx(I, J) * 1024; };
   for (int i = tid; i < Dp; i += 512) yv[i] = slot[(int64_t)NT * 1024 + i];
@@ -833,7 +843,7 @@ __global__ void __launch_bounds__(512)
   };
 
 #pragma unroll 1
-  for (int p = 0; p < T; ++p) {
+  for (int p = 0; p < te; ++p) {
     // ---- A: row p of L (the thread's loads issued four at a time, each
     // unconditional -- past the row it re-reads tile (p, 0) and drops it --
     // so a panel costs two HBM round trips, not one per float4) ----
@@ -930,7 +940,7 @@ __global__ void __launch_bounds__(512)
         r += __shfl_xor(r, 32);
         if (hi == 0) rv[lo] = yv[32 * p + lo] - r;
       }
-      if (p + wave < T) acc0 = panel_sum(p + wave, p);  // first panel tile
+      if (p + wave < te) acc0 = panel_sum(p + wave, p);  // first panel tile
     }
     __syncthreads();
     // ---- C ----
@@ -943,7 +953,7 @@ __global__ void __launch_bounds__(512)
     } else {
       // first tile from its B-phase sum, the rest sum-then-finish (L_pp^-1 is ready)
 #pragma unroll 1
-      for (int I = p + wave; I < T; I += NW - 1) {
+      for (int I = p + wave; I < te; I += NW - 1) {
         const f32x16 cI = I == p + wave ? acc0 : panel_sum(I, p);
         f32x16 l = f32x16{0.f};
 #pragma unroll
@@ -955,11 +965,11 @@ __global__ void __launch_bounds__(512)
     }
     __syncthreads();
   }
-  wide_back_subst<T>(slot, yv, xv, part, wave, lo, hi);
+  wide_back_subst<T>(slot, yv, xv, part, wave, lo, hi, te);
   // slot_out: the solution of slot b into out[Dp b ..) (the history-space
   // wide bucket's S systems), else into the entity's row
   const int64_t orow = slot_out ? (int64_t)blockIdx.x : e;
-  for (int i = tid; i < Dp; i += 512) a.out[orow * Dp + i] = xv[i];
+  for (int i = tid; i < Dp; i += 512) a.out[orow * Dp + i] = i < 32 * te ? xv[i] : 0.0f;
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
@@ -1557,7 +1567,7 @@ hipError_t launch_wide_gram_final(int Dp, const float* gslabs, int64_t ngroup, f
 }
 
 hipError_t launch_wide_chol_slots(const QueueRec* order, int64_t n, float* slots, float* out,
-                                  unsigned long long* fail, hipStream_t s) {
+                                  unsigned long long* fail, int quirk_v, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   static bool attr = false;
   if (!attr) {
@@ -1572,7 +1582,7 @@ hipError_t launch_wide_chol_slots(const QueueRec* order, int64_t n, float* slots
   a.out = out;
   a.fail = fail;
   hipLaunchKernelGGL(wide_chol_kernel<16>, dim3((unsigned)n), dim3(512), wide_chol_lds_bytes(512),
-                     s, a, (int64_t)0, slots, 1);
+                     s, a, (int64_t)0, slots, quirk_v ? 2 : 1);
   return hipGetLastError();
 }
 
