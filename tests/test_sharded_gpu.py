@@ -103,9 +103,10 @@ def ml1m_csr(ml1m):
     return tr.max_user + 1, tr.max_item + 1, up, uc, ip, ic
 
 
-@pytest.mark.parametrize("world", [2, 3, 8])
-@pytest.mark.parametrize("dim", [8, 32, 64, 256, 512])
+@pytest.mark.parametrize("world,dim", [(w, d) for w in (2, 3, 8) for d in (8, 32, 64, 256, 512)]
+                         + [(2, 1000), (3, 1000)])
 def test_sharded_ials_matches_single(ml1m_csr, world, dim):
+    # dim 1000 (Dp = 1024): the history-space wide bucket (256 < h_eff <= 512)
     nu, ni, up, uc, ip, ic = ml1m_csr
     reg, w = 0.003, 0.1
     single = _contexts(1, dim, nu, ni, up, uc, ip, ic)
