@@ -224,7 +224,9 @@ int frecsys_pp_predict(frecsys_ctx* ctx, int32_t side);
  * rank replays the other ranks' prediction updates from them, so the
  * prediction vector and the embeddings are bitwise the single-rank ones;
  * without a communicator (external exchange) the caller copies the other
- * ranks' rows in (frecsys_set_embeddings) and calls frecsys_pp_sync.
+ * ranks' rows in (frecsys_set_embeddings) and calls frecsys_pp_sync; until
+ * it does, a further frecsys_pp_step or frecsys_pp_predict on the context
+ * fails with FRECSYS_ERR_INVALID ("pp_sync pending").
  * residual (may be NULL): sum of squared block deltas (over every rank's
  * rows with RCCL, this rank's rows otherwise). */
 int frecsys_pp_step(frecsys_ctx* ctx, int32_t side, int32_t start, int32_t end,
