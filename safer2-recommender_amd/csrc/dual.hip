@@ -936,33 +936,38 @@ __global__ void __launch_bounds__(256) dual_wide_s_kernel(const bf16x8* zs_all, 
     for (int v = 0; v < 2; ++v) acc[u][v] = f32x16{0.f};
   const bool live = I0 < te && J0 < te && !(BI == BJ && J0 > I0 + 1);
   if (live) {
+    // 32-bit element offsets inside the entity's fragment block (3 MB at
+    // Dp = 1024): granule (kb, p, hh, j) at ((kb * 3 + p) * 2 + hh) * 512 + j
+    const int oa = hi * kWideHP + 32 * I0 + lo, ob = hi * kWideHP + 32 * J0 + lo;
     bf16x8 fa[2][3], fb[2][3];
     auto load = [&](int kb, bf16x8(&A)[2][3], bf16x8(&B)[2][3]) __attribute__((always_inline)) {
+      const int base = kb * 6 * kWideHP;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-          A[u][p] = zs[wz_gran(kb, p, hi, 32 * (I0 + u) + lo)];
-          B[u][p] = zs[wz_gran(kb, p, hi, 32 * (J0 + u) + lo)];
+          A[u][p] = zs[base + 2 * p * kWideHP + oa + 32 * u];
+          B[u][p] = zs[base + 2 * p * kWideHP + ob + 32 * u];
         }
     };
+    // two k16 steps per iteration, each step's fragments loaded one step
+    // ahead into the other register set (no copies between the sets)
+    bf16x8 ga[2][3], gb[2][3];
     load(0, fa, fb);
 #pragma unroll 1
-    for (int kb = 0; kb < Dp / 16; ++kb) {
-      bf16x8 na[2][3], nb[2][3];
-      if (kb + 1 < Dp / 16) load(kb + 1, na, nb);
+    for (int kb = 0; kb < Dp / 16; kb += 2) {
+      load(kb + 1, ga, gb);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int v = 0; v < 2; ++v)
           if (!(BI == BJ && J0 + v > I0 + u)) acc[u][v] = mfma_x6(fa[u], fb[v], acc[u][v]);
+      if (kb + 2 < Dp / 16) load(kb + 2, fa, fb);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          fa[u][p] = na[u][p];
-          fb[u][p] = nb[u][p];
-        }
+        for (int v = 0; v < 2; ++v)
+          if (!(BI == BJ && J0 + v > I0 + u)) acc[u][v] = mfma_x6(ga[u], gb[v], acc[u][v]);
     }
   }
 #pragma unroll
