@@ -59,6 +59,10 @@ fh = None
 SHAPES = synthetic = None
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix peak (spec)
+# the products run as 6 bf16 MFMAs per fp32-accurate product (common.h
+# mfma_x6): their own ceiling is the dense bf16 peak / 6, in fp32 flops
+PEAK_BF16_TFLOPS = 2500.0
+PEAK_SPLIT_BF16_TFLOPS = PEAK_BF16_TFLOPS / 6.0
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 # BASELINE.json configs; flags are the run_model flags (README.md lines cited).
@@ -442,6 +446,9 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
                                 "MFMA SYRK + fp32 dataflow Cholesky)"),
                      "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": traffic,
+                     # the same work against the split-bf16 ceiling the kernels run at
+                     "peak_split_bf16": PEAK_SPLIT_BF16_TFLOPS,
+                     "frac_split_bf16": achieved_tf / PEAK_SPLIT_BF16_TFLOPS,
                      "traffic_source": traffic_src,
                      "avg_launch_ms": avg_ms, "flops_per_launch": flops},
         "paths": paths,
