@@ -90,6 +90,12 @@ DEFAULT_EXTRAS = ("safer2_ml20m_d256", "ials_msd_d512")
 DEFAULT_EXTRAS_N1 = ("safer2_2m500k_d1024",)
 
 
+def default_extras(world):
+    """The extra workloads of a default run: the other BASELINE configs, and
+    config 5 (2M x 500K, d = 1024) on one GPU only."""
+    return ",".join(DEFAULT_EXTRAS + (DEFAULT_EXTRAS_N1 if world == 1 else ()))
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -522,7 +528,7 @@ def main():
                         args.steps, args.warmup, args.cpu_seconds)
     extras = []
     if args.extras is None:
-        args.extras = ",".join(DEFAULT_EXTRAS + (DEFAULT_EXTRAS_N1 if world == 1 else ()))
+        args.extras = default_extras(world)
     for name in [x for x in args.extras.split(",") if x and x != args.workload]:
         steps = min(args.extra_steps, WORKLOADS[name].get("max_extra_steps", args.extra_steps))
         extras.append(run_workload(name, args, world, rank, local_rank, dist, data_cache,

@@ -45,3 +45,14 @@ def test_world_size_mismatch_refused():
 def test_frecsys_env_refused():
     r = _run(["--gpus", "1"], FRECSYS_DUAL="0")
     assert r.returncode != 0 and "refusing" in r.stderr
+
+
+def test_default_extras_config5_at_one_gpu_only():
+    import bench
+    one = bench.default_extras(1).split(",")
+    many = bench.default_extras(8).split(",")
+    assert "safer2_2m500k_d1024" in one and "safer2_2m500k_d1024" not in many
+    assert set(many) == {"safer2_ml20m_d256", "ials_msd_d512"}
+    assert bench.WORKLOADS["safer2_2m500k_d1024"]["max_extra_steps"] == 2
+    # every default extra is a BASELINE config the bench knows
+    assert all(w in bench.WORKLOADS for w in one)
