@@ -878,34 +878,43 @@ __global__ void __launch_bounds__(512) dual_wide_z_kernel(DualArgs a, bf16x8* zs
   // rows past the entity's last tile are never read (dual_wide_s_kernel)
   if (tid >= 32 * ((ntot + 31) / 32)) return;
   const float* row = a.Xrot + (int64_t)id * Dp;
-  float4 y[4], yn[4];
+  // the row's 16-column steps through a 4-deep register ring: the loads of
+  // steps kb+1 .. kb+3 are in flight under step kb's recurrence (the loop
+  // unrolled by 4 so every ring slot is a fixed set of registers; Dp / 16 is
+  // a multiple of 4)
+  constexpr int R = 4;
+  const int NK = Dp / 16;
+  float4 ring[R][4];
+  auto ld = [&](int kb, float4(&dst)[4]) __attribute__((always_inline)) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) y[q] = *reinterpret_cast<const float4*>(row + 4 * q);
+    for (int q = 0; q < 4; ++q) dst[q] = *reinterpret_cast<const float4*>(row + 16 * kb + 4 * q);
+  };
+#pragma unroll
+  for (int j = 0; j < R - 1; ++j) ld(j, ring[j]);
   float z = 0.0f;
 #pragma unroll 1
-  for (int kb = 0; kb < Dp / 16; ++kb) {
-    if (kb + 1 < Dp / 16) {
+  for (int kb0 = 0; kb0 < NK; kb0 += R) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) yn[q] = *reinterpret_cast<const float4*>(row + 16 * (kb + 1) + 4 * q);
-    }
+    for (int j = 0; j < R; ++j) {
+      const int kb = kb0 + j;
+      if (kb + R - 1 < NK) ld(kb + R - 1, ring[(j + R - 1) % R]);
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      float v[8];
+      for (int hh = 0; hh < 2; ++hh) {
+        float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const float4 y4 = y[2 * hh + (u >> 2)];
-        const float yv = (u & 3) == 0 ? y4.x : (u & 3) == 1 ? y4.y : (u & 3) == 2 ? y4.z : y4.w;
-        const int k = 16 * kb + 8 * hh + u;
-        z = yv - lsub[k] * z;
-        v[u] = (cj * z) * dsq[k];
+        for (int u = 0; u < 8; ++u) {
+          const float4 y4 = ring[j][2 * hh + (u >> 2)];
+          const float yv = (u & 3) == 0 ? y4.x : (u & 3) == 1 ? y4.y : (u & 3) == 2 ? y4.z : y4.w;
+          const int k = 16 * kb + 8 * hh + u;
+          z = yv - lsub[k] * z;
+          v[u] = (cj * z) * dsq[k];
+        }
+        bf16x8 f[3];
+        split3x8(v, f);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) zs[wz_gran(kb, p, hh, tid)] = f[p];
       }
-      bf16x8 f[3];
-      split3x8(v, f);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) zs[wz_gran(kb, p, hh, tid)] = f[p];
     }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) y[q] = yn[q];
   }
 }
 
@@ -936,38 +945,33 @@ __global__ void __launch_bounds__(256) dual_wide_s_kernel(const bf16x8* zs_all, 
     for (int v = 0; v < 2; ++v) acc[u][v] = f32x16{0.f};
   const bool live = I0 < te && J0 < te && !(BI == BJ && J0 > I0 + 1);
   if (live) {
-    // 32-bit element offsets inside the entity's fragment block (3 MB at
-    // Dp = 1024): granule (kb, p, hh, j) at ((kb * 3 + p) * 2 + hh) * 512 + j
-    const int oa = hi * kWideHP + 32 * I0 + lo, ob = hi * kWideHP + 32 * J0 + lo;
     bf16x8 fa[2][3], fb[2][3];
     auto load = [&](int kb, bf16x8(&A)[2][3], bf16x8(&B)[2][3]) __attribute__((always_inline)) {
-      const int base = kb * 6 * kWideHP;
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-          A[u][p] = zs[base + 2 * p * kWideHP + oa + 32 * u];
-          B[u][p] = zs[base + 2 * p * kWideHP + ob + 32 * u];
+          A[u][p] = zs[wz_gran(kb, p, hi, 32 * (I0 + u) + lo)];
+          B[u][p] = zs[wz_gran(kb, p, hi, 32 * (J0 + u) + lo)];
         }
     };
-    // two k16 steps per iteration, each step's fragments loaded one step
-    // ahead into the other register set (no copies between the sets)
-    bf16x8 ga[2][3], gb[2][3];
     load(0, fa, fb);
 #pragma unroll 1
-    for (int kb = 0; kb < Dp / 16; kb += 2) {
-      load(kb + 1, ga, gb);
+    for (int kb = 0; kb < Dp / 16; ++kb) {
+      bf16x8 na[2][3], nb[2][3];
+      if (kb + 1 < Dp / 16) load(kb + 1, na, nb);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int v = 0; v < 2; ++v)
           if (!(BI == BJ && J0 + v > I0 + u)) acc[u][v] = mfma_x6(fa[u], fb[v], acc[u][v]);
-      if (kb + 2 < Dp / 16) load(kb + 2, fa, fb);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
-          if (!(BI == BJ && J0 + v > I0 + u)) acc[u][v] = mfma_x6(ga[u], gb[v], acc[u][v]);
+        for (int p = 0; p < 3; ++p) {
+          fa[u][p] = na[u][p];
+          fb[u][p] = nb[u][p];
+        }
     }
   }
 #pragma unroll
