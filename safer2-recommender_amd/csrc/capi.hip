@@ -158,10 +158,11 @@ struct frecsys_ctx {
   bool wide_presplit = true;
   // FRECSYS_WIDE_WS_MB: the budget of EACH of the wide workspaces (the batch
   // workspace of A tiles, the long-history slabs, the history-space wide
-  // bucket): up to three times this in device memory (24 GB of 288 at the
-  // default; 8 GB instead of 4 measured 0.6 % faster at MSD and config 5 --
-  // fewer, fuller batches)
-  int64_t wide_ws_mb = 8192;
+  // bucket), each allocated only as large as its batch needs: up to three
+  // times this in device memory (48 GB of 288 at the default; 8 GB instead of
+  // 4 measured 0.6 % faster at MSD and config 5, 16 GB another 1.5 % at
+  // config 5 -- fewer, fuller batches)
+  int64_t wide_ws_mb = 16384;
   // long-history split of the d-space solve
   int split_rows = 4096;         // rows per partial SYRK (FRECSYS_SPLIT_ROWS, 0 = off; swept 512..4096 at ML-20M d=256: 4096 best)
   std::vector<int2> h_split;
