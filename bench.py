@@ -19,8 +19,9 @@ T = max over ranks of the K-epoch wall time.  sec_per_epoch = T / K.
 `workloads` carries the same measurement for BASELINE configs[2] (SAFER2 d=256
 ML-20M-shaped, README.md:79 flags, pd=1 xi=5 use_snr=1 sampling_ratio=0.1) and
 configs[3] (iALS d=512 MSD-shaped, README.md:105), each with its own roofline,
-gather roofline and cpu_baseline; `--workload` runs one of them (or config 5,
-SAFER2 d=1024 2M x 500K, which is opt-in: its data alone takes minutes).
+gather roofline and cpu_baseline, and configs[4] (SAFER2 d=1024 2M x 500K,
+README.md:100; 2 timed epochs) -- all three at every N; `--workload` runs
+one of them as the headline.
 
 roofline: the dominant kernel of the workload, priced against the fp32 MFMA peak
 (157.3 TFLOP/s; the algorithm is fp32 and compute-bound): algorithmic flops per
@@ -84,16 +85,27 @@ WORKLOADS = {
         max_extra_steps=2),  # ~1.6 s epochs after ~40 s of data generation
 }
 HEADLINE = "ials_ml20m_d256"
-DEFAULT_EXTRAS = ("safer2_ml20m_d256", "ials_msd_d512")
-# measured after the others on one GPU only (a strong-scaling N>1 run keeps
-# to the three smaller configs so the driver's scaling sweep stays short)
-DEFAULT_EXTRAS_N1 = ("safer2_2m500k_d1024",)
+# the other BASELINE configs, at every N: configs[3] and configs[4] are defined
+# on 8 GPUs (BASELINE.json), so the driver's N = 1, 2, 4, 8 sweep measures
+# them all; config 5 last (its data takes ~40 s per rank)
+DEFAULT_EXTRAS = ("safer2_ml20m_d256", "ials_msd_d512", "safer2_2m500k_d1024")
 
 
 def default_extras(world):
-    """The extra workloads of a default run: the other BASELINE configs, and
-    config 5 (2M x 500K, d = 1024) on one GPU only."""
-    return ",".join(DEFAULT_EXTRAS + (DEFAULT_EXTRAS_N1 if world == 1 else ()))
+    """The extra workloads of a default run at any world size: BASELINE
+    configs 3, 4 and 5 (the CPU baseline is timed at N = 1 only)."""
+    del world
+    return ",".join(DEFAULT_EXTRAS)
+
+
+def launch_plan(args, world):
+    """What a run of these arguments measures: the rank launch (None when this
+    process is already a rank), the headline and the extra workloads."""
+    extras = args.extras if args.extras is not None else default_extras(world)
+    return {"launch": launch_command(args) if world_from_env(args) is None else None,
+            "n_gpus": world, "workload": args.workload,
+            "extras": [x for x in extras.split(",") if x and x != args.workload],
+            "cpu_baseline": world == 1 and args.cpu_seconds > 0}
 
 
 def parse():
@@ -104,8 +116,7 @@ def parse():
     ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
     ap.add_argument("--extras", default=None,
                     help="comma-separated extra workloads measured after the headline "
-                         "('' for none; default: the other BASELINE configs, the 2M x 500K "
-                         "d=1024 one at N=1 only)")
+                         "('' for none; default: the other BASELINE configs 3, 4, 5)")
     ap.add_argument("--extra-steps", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU-baseline sample duration per workload (0 disables)")
@@ -113,7 +124,8 @@ def parse():
                     help="run although FRECSYS_* variables are set (recorded in the line)")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--print-launch", action="store_true",
-                    help="print the N-rank launch command bench.py would run and exit")
+                    help="print the launch plan (the N-rank command bench.py would run, the "
+                         "headline and extra workloads) as JSON and exit")
     return ap.parse_args()
 
 
@@ -502,15 +514,11 @@ def main():
         sys.exit(f"bench.py: refusing to run with {sorted(env)} set (profiling path selectors; "
                  f"pass --allow-env to run anyway, recorded in the line)")
     ranks = world_from_env(args)
-    if ranks is None:  # launch the N ranks (children) and exit with their status
-        cmd = launch_command(args)
-        if args.print_launch:
-            print(json.dumps(cmd))
-            return
-        sys.exit(subprocess.run(cmd).returncode)
     if args.print_launch:
-        print(json.dumps(None))
+        print(json.dumps(launch_plan(args, args.gpus)))
         return
+    if ranks is None:  # launch the N ranks (children) and exit with their status
+        sys.exit(subprocess.run(launch_command(args)).returncode)
     world, rank, local_rank = ranks
     import frecsys_hip as fh_mod
     from frecsys_hip import data as fh_data
@@ -531,8 +539,12 @@ def main():
         args.extras = default_extras(world)
     for name in [x for x in args.extras.split(",") if x and x != args.workload]:
         steps = min(args.extra_steps, WORKLOADS[name].get("max_extra_steps", args.extra_steps))
-        extras.append(run_workload(name, args, world, rank, local_rank, dist, data_cache,
-                                   steps, 1, args.cpu_seconds))
+        try:
+            extras.append(run_workload(name, args, world, rank, local_rank, dist, data_cache,
+                                       steps, 1, args.cpu_seconds))
+        except Exception as e:  # an extra never takes the headline line down with it
+            log(f"[bench] {name} failed on rank {rank}: {e!r}")
+            extras.append({"workload": name, "error": repr(e)})
     if rank == 0:
         spec = WORKLOADS[args.workload]
         line = {

@@ -220,21 +220,49 @@ int frecsys_pp_predict(frecsys_ctx* ctx, int32_t side);
  * alpha as for frecsys_solve_side, G[other] the omega-weighted Gramian for
  * WEIGHTED_V).  Updates the block of the rows and their predictions.
  * At world > 1 (USER / ITEM) each rank solves its own shard of the rows
- * (frecsys_shard_range); with RCCL the rows are then all-gathered and every
- * rank replays the other ranks' prediction updates from them, so the
- * prediction vector and the embeddings are bitwise the single-rank ones;
- * without a communicator (external exchange) the caller copies the other
- * ranks' rows in (frecsys_set_embeddings) and calls frecsys_pp_sync; until
- * it does, a further frecsys_pp_step or frecsys_pp_predict on the context
- * fails with FRECSYS_ERR_INVALID ("pp_sync pending").
+ * (frecsys_shard_range).  With an in-call exchange -- RCCL, or the caller's
+ * transport (frecsys_set_transport): one code path, only the transport call
+ * differs -- the rows are then all-gathered, every rank replays the other
+ * ranks' prediction updates from them, takes the same NOT_SPD verdict (a
+ * min over ranks) and sums every rank's per-row residuals in the
+ * single-rank order, so the embeddings, the prediction vector and the
+ * residual are bitwise the single-rank ones.  Every rank must make the same
+ * sequence of calls.  Without either (external exchange, no transport) the
+ * caller copies the other ranks' rows in (frecsys_set_embeddings) and calls
+ * frecsys_pp_sync -- also after a step that returned FRECSYS_ERR_NOT_SPD,
+ * whose updates were applied; until it does, a further frecsys_pp_step or
+ * frecsys_pp_predict on the context fails with FRECSYS_ERR_INVALID
+ * ("pp_sync pending").  A step that fails for another reason leaves nothing
+ * pending; its rows are then undefined (rerun frecsys_pp_predict).
  * residual (may be NULL): sum of squared block deltas (over every rank's
- * rows with RCCL, this rank's rows otherwise). */
+ * rows with an in-call exchange, this rank's rows otherwise). */
 int frecsys_pp_step(frecsys_ctx* ctx, int32_t side, int32_t start, int32_t end,
                     const frecsys_solve_params* params, double* residual);
 /* External-exchange completion of a sharded frecsys_pp_step on `side`: after
  * the other ranks' rows were set, apply their block updates to this rank's
  * prediction vector.  No reference counterpart (the sharded path is new). */
 int frecsys_pp_sync(frecsys_ctx* ctx, int32_t side);
+/* The prediction vector of the training tuples (side USER) or of the EVAL
+ * rows (side EVAL), [nnz of the side] floats, indexed by rating index. */
+int frecsys_pp_get_predictions(frecsys_ctx* ctx, int32_t side, float* host);
+/* Caller-provided transport for the exchanges a sharded call makes inside
+ * itself when the context has no RCCL communicator (frecsys_comm_init with
+ * id NULL): the same points in the same order as the RCCL calls (today:
+ * frecsys_pp_step).  Each callback returns 0 on success; every rank calls
+ * them in the same order.
+ *   allgather_rows: `rows` is a host copy of a whole per-row table of `side`
+ *     (n_rows x ld floats, row-major); on entry rows [lo, hi) hold this
+ *     rank's values, on return every row must hold its owner rank's values
+ *     (an all-gather with the uneven counts of frecsys_shard_range);
+ *   allreduce_min_u64: *value becomes the minimum over the ranks.
+ * t == NULL removes the transport.  No reference counterpart. */
+typedef struct frecsys_transport {
+  void* user;
+  int (*allgather_rows)(void* user, int32_t side, float* rows, int64_t n_rows, int64_t ld,
+                        int64_t lo, int64_t hi);
+  int (*allreduce_min_u64)(void* user, uint64_t* value);
+} frecsys_transport;
+int frecsys_set_transport(frecsys_ctx* ctx, const frecsys_transport* t);
 /* Fold-in evaluation ranking (replaces the scoring + top-K of
  * EvaluateDatasetInternal / EvaluateUser, recommender.h:78-199): for every
  * row r of the EVAL side, scores s = V u_r over all items (fp32), the items
@@ -263,11 +291,22 @@ int frecsys_snapshot_residual(frecsys_ctx* ctx, int32_t side, double* sq);
  *                     history-space pivot failure (a silent slow path);
  *   "tagged_timeouts" device polls of the tagged-word exchange of the
  *                     tridiagonalisation that timed out (each one poisons
- *                     the basis and forces a rerun).
+ *                     the basis and forces a rerun);
+ *   "ws_shrinks"      wide workspaces (d = 257..1024) cut below their
+ *                     budget by a failed device allocation: a halved batch,
+ *                     fewer long-history slabs, or the register-staged SYRK
+ *                     instead of the pre-split table -- results unchanged.
  * No reference counterpart (diagnostics of the MI355X path). */
 int frecsys_counter(frecsys_ctx* ctx, const char* what, int64_t* value);
 /* Block until all queued device work is done (all calls already do). */
 int frecsys_synchronize(frecsys_ctx* ctx);
+/* Free the wide-dim workspaces (batch workspace of A tiles, long-history
+ * slabs, pre-split table, history-space wide bucket); the next solve sizes
+ * them again within FRECSYS_WIDE_WS_MB and a quarter of the then free device
+ * memory each.  For a caller that needs the device memory between phases
+ * (evaluation, another model).  No reference counterpart: the reference's
+ * per-thread Eigen temporaries are freed per entity. */
+int frecsys_release_workspaces(frecsys_ctx* ctx);
 
 /* ---- profiling hooks (bench.py) ----
  * Kernel time accumulated with HIP events recorded on the library's

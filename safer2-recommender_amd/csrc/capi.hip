@@ -131,6 +131,13 @@ struct frecsys_ctx {
   float* d_pp_old = nullptr;
   size_t cap_pp_old = 0;
   int pp_old_side = -1, pp_old_start = 0, pp_old_bw = 0;
+  // external-exchange transport (frecsys_set_transport): the in-call
+  // exchanges of a sharded call without a communicator
+  frecsys_transport transport{};
+  bool has_transport = false;
+  std::vector<int32_t> pp_order_all[2];  // every row of the side by decreasing h (stable)
+  float* d_resid_e = nullptr;            // per-entity residuals [n] of a sharded pp_step
+  size_t cap_resid_e = 0;
   float* d_rows = nullptr;       // train stats: per-row values
   size_t cap_rows = 0;
   float* d_gstat = nullptr;      // train stats: U^T U, V^T V
@@ -158,11 +165,18 @@ struct frecsys_ctx {
   bool wide_presplit = true;
   // FRECSYS_WIDE_WS_MB: the budget of EACH of the wide workspaces (the batch
   // workspace of A tiles, the long-history slabs, the history-space wide
-  // bucket), each allocated only as large as its batch needs: up to three
-  // times this in device memory (48 GB of 288 at the default; 8 GB instead of
+  // bucket), each allocated only as large as its batch needs (8 GB instead of
   // 4 measured 0.6 % faster at MSD and config 5, 16 GB another 1.5 % at
-  // config 5 -- fewer, fuller batches)
+  // config 5 -- fewer, fuller batches).  Each is also capped at a quarter of
+  // the device memory free when it is sized (ws_budget), and a failed
+  // allocation halves its batch instead of failing the call (ensure_batch);
+  // the pre-split table of the other side ((n_other + 1) (6 Dp + 128) B:
+  // 12.6 GB for config 5's 2M users) falls back to the register-staged SYRK
+  // (bit-identical) when it does not fit.  At the default, the three
+  // workspaces and the table take <= 61 GB of 288 at config 5.
   int64_t wide_ws_mb = 16384;
+  bool ws_free_cap = true;   // FRECSYS_WS_FREE_CAP=0: no free-memory cap (tests of the OOM path)
+  int64_t ws_shrinks = 0;    // allocations cut by a failed hipMalloc (frecsys_counter "ws_shrinks")
   // long-history split of the d-space solve
   int split_rows = 4096;         // rows per partial SYRK (FRECSYS_SPLIT_ROWS, 0 = off; swept 512..4096 at ML-20M d=256: 4096 best)
   std::vector<int2> h_split;
@@ -295,6 +309,61 @@ int ensure(frecsys_ctx* c, T** p, size_t* cap, size_t count) {
   return FRECSYS_OK;
 }
 
+// ensure() that reports an out-of-memory hipMalloc instead of failing: *oom
+// is set, *p left null and HIP's sticky last error cleared (the next launch
+// check would otherwise see it).
+template <typename T>
+int try_ensure(frecsys_ctx* c, T** p, size_t* cap, size_t count, bool* oom) {
+  *oom = false;
+  if (*cap >= count && *p) return FRECSYS_OK;
+  if (*p) HIP_TRY(c, hipFree(*p));
+  *p = nullptr;
+  *cap = 0;
+  const hipError_t e = hipMalloc((void**)p, sizeof(T) * std::max<size_t>(count, 1));
+  if (e == hipSuccess) {
+    *cap = count;
+    return FRECSYS_OK;
+  }
+  *p = nullptr;
+  (void)hipGetLastError();
+  if (e != hipErrorOutOfMemory)
+    return fail(c, FRECSYS_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+  *oom = true;
+  return FRECSYS_OK;
+}
+
+// Bytes one wide workspace may take now: FRECSYS_WIDE_WS_MB, capped at a
+// quarter of the device memory that is free (plus what the workspace
+// already holds), so several contexts or other tenants of the device leave
+// each other room.
+size_t ws_budget(frecsys_ctx* c, size_t held) {
+  size_t b = (size_t)c->wide_ws_mb << 20;
+  size_t fr = 0, tot = 0;
+  if (c->ws_free_cap) {
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+      b = std::min(b, (fr + held) / 4);
+    else
+      (void)hipGetLastError();
+  }
+  return b;
+}
+
+// A workspace of *batch slots of `per` elements: a failed hipMalloc halves
+// the batch (counted in ws_shrinks) until one slot does not fit either.
+// Entities are independent, so the batch size never changes a result.
+template <typename T>
+int ensure_batch(frecsys_ctx* c, T** p, size_t* cap, size_t per, int64_t* batch) {
+  while (true) {
+    bool oom = false;
+    int rc = try_ensure(c, p, cap, per * (size_t)*batch, &oom);
+    if (rc || !oom) return rc;
+    if (*batch <= 1)
+      return fail(c, FRECSYS_ERR_HIP, "hipMalloc: out of memory for one workspace slot");
+    *batch = (*batch + 1) / 2;
+    ++c->ws_shrinks;
+  }
+}
+
 bool valid_side(int side) { return side >= 0 && side <= 2; }
 
 // Contiguous nnz-balanced split: rank r gets rows whose prefix nnz falls in
@@ -413,33 +482,49 @@ HeffSums heff_sums(frecsys_ctx* c, int side, bool vq, int64_t lo, int64_t hi) {
 // Long-history split of the d-space queue prefix [0, n): entities with
 // more than 2*C assembly rows get their SYRK cut into C-row slabs done by
 // separate workgroups (launch_split_syrk / wide_syrk2_kernel<2>) before the
-// solve; at most max_slabs slabs of slab_floats each (longest entities first).
+// solve; at most max_slabs slabs of slab_floats each (longest entities first;
+// shrink: fewer when their allocation fails -- only where the split does not
+// change the sums' order, the wide dims).
 int plan_split(frecsys_ctx* c, const std::vector<int32_t>& hs, int64_t n,
                const std::function<int64_t(int64_t)>& heff, SolveArgs* a, int64_t C,
-               size_t slab_floats, int64_t max_slabs, hipStream_t s) {
+               size_t slab_floats, int64_t max_slabs, hipStream_t s, bool shrink = false) {
   a->split = nullptr;
   a->n_split = 0;
   a->slabs = nullptr;
   a->work = nullptr;
   a->n_work = 0;
   if (c->split_rows <= 0 || C <= 0 || c->Dp < 32) return FRECSYS_OK;
-  c->h_split.clear();
-  c->h_work.clear();
   int32_t slab = 0;
-  for (int64_t i = 0; i < n && heff(hs[i]) > 2 * C; ++i) {
-    const int64_t ne = heff(hs[i]);
-    if (slab + (ne + C - 1) / C > max_slabs) break;
-    const int32_t first = slab;
-    for (int64_t k = 0; k < ne; k += C)
-      c->h_work.push_back(SplitWork{(int32_t)i, (int32_t)k, (int32_t)std::min(ne, k + C), slab++});
-    c->h_split.push_back(int2{first, slab - first});
+  while (true) {
+    c->h_split.clear();
+    c->h_work.clear();
+    slab = 0;
+    for (int64_t i = 0; i < n && heff(hs[i]) > 2 * C; ++i) {
+      const int64_t ne = heff(hs[i]);
+      if (slab + (ne + C - 1) / C > max_slabs) break;
+      const int32_t first = slab;
+      for (int64_t k = 0; k < ne; k += C)
+        c->h_work.push_back(SplitWork{(int32_t)i, (int32_t)k, (int32_t)std::min(ne, k + C), slab++});
+      c->h_split.push_back(int2{first, slab - first});
+    }
+    if (c->h_split.empty()) return FRECSYS_OK;
+    if (!shrink) {
+      int rc = ensure(c, &c->d_slabs, &c->cap_slabs, (size_t)slab * slab_floats);
+      if (rc) return rc;
+      break;
+    }
+    // the wide dims (split and unsplit SYRKs are bit-identical there): fewer
+    // slabs when the allocation fails
+    bool oom = false;
+    int rc = try_ensure(c, &c->d_slabs, &c->cap_slabs, (size_t)slab * slab_floats, &oom);
+    if (rc) return rc;
+    if (!oom) break;
+    ++c->ws_shrinks;
+    max_slabs = slab / 2;
   }
-  if (c->h_split.empty()) return FRECSYS_OK;
   int rc = ensure(c, &c->d_split, &c->cap_split, c->h_split.size());
   if (rc) return rc;
   rc = ensure(c, &c->d_work, &c->cap_work, c->h_work.size());
-  if (rc) return rc;
-  rc = ensure(c, &c->d_slabs, &c->cap_slabs, (size_t)slab * slab_floats);
   if (rc) return rc;
   // on the solve's own stream: a blocking hipMemcpy went through a queue that
   // could be FIFO-behind the basis chain, holding the d-space launch back
@@ -651,6 +736,46 @@ int allgather_rows(frecsys_ctx* c, float* base, int side, int64_t ld) {
     NCCL_TRY(c, ncclBroadcast(p, p, cnt, ncclFloat, r, c->comm, c->stream));
   }
   NCCL_TRY(c, ncclGroupEnd());
+  return FRECSYS_OK;
+}
+
+// The exchanges a sharded call makes inside itself, one code path for both
+// transports: RCCL (a communicator) or the caller's callbacks
+// (frecsys_set_transport).  Without either (world 1, or external exchange
+// with no transport) a call does not exchange; the caller completes it.
+bool in_call_exchange(const frecsys_ctx* c) { return c->world > 1 && (c->comm || c->has_transport); }
+
+// All-gather of a per-row device table of `side` (ld floats per row).
+int xchg_rows(frecsys_ctx* c, float* base, int side, int64_t ld) {
+  if (c->comm) return allgather_rows(c, base, side, ld);
+  if (!c->has_transport) return FRECSYS_OK;
+  const int64_t n = c->n[side];
+  std::vector<float> h((size_t)std::max<int64_t>(n * ld, 1));
+  if (n) HIP_TRY(c, hipMemcpyAsync(h.data(), base, sizeof(float) * n * ld, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  int64_t lo, hi;
+  shard(c, side, &lo, &hi);
+  if (c->transport.allgather_rows(c->transport.user, side, h.data(), n, ld, lo, hi) != 0)
+    return fail(c, FRECSYS_ERR_RCCL, "transport: allgather_rows failed");
+  if (n) HIP_TRY(c, hipMemcpyAsync(base, h.data(), sizeof(float) * n * ld, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+// In-place minimum over ranks of one device u64.
+int xchg_min_u64(frecsys_ctx* c, unsigned long long* dval) {
+  if (c->comm) {
+    NCCL_TRY(c, ncclAllReduce(dval, dval, 1, ncclUint64, ncclMin, c->comm, c->stream));
+    return FRECSYS_OK;
+  }
+  if (!c->has_transport) return FRECSYS_OK;
+  uint64_t v = 0;
+  HIP_TRY(c, hipMemcpyAsync(&v, dval, sizeof(v), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (c->transport.allreduce_min_u64(c->transport.user, &v) != 0)
+    return fail(c, FRECSYS_ERR_RCCL, "transport: allreduce_min_u64 failed");
+  HIP_TRY(c, hipMemcpyAsync(dval, &v, sizeof(v), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FRECSYS_OK;
 }
 
@@ -1009,6 +1134,7 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   }
   if (const char* v = getenv("FRECSYS_WIDE_WS_MB")) c->wide_ws_mb = std::max(1, atoi(v));
   if (const char* v = getenv("FRECSYS_WIDE_PRESPLIT")) c->wide_presplit = atoi(v) != 0;
+  if (const char* v = getenv("FRECSYS_WS_FREE_CAP")) c->ws_free_cap = atoi(v) != 0;
   // the wide dims add the wide bucket (256 < h_eff <= 512, dual.hip)
   const int max_h_cap = Dp >= 512 ? kDualWideMaxH : 32 * kDualMaxTiles;
   c->dual_max_h = std::min(c->dual_max_h, max_h_cap);
@@ -1089,6 +1215,7 @@ void frecsys_ctx_destroy(frecsys_ctx* c) {
     if (c->d_pred[s]) (void)hipFree(c->d_pred[s]);
   }
   if (c->d_resid) (void)hipFree(c->d_resid);
+  if (c->d_resid_e) (void)hipFree(c->d_resid_e);
   if (c->d_gstat) (void)hipFree(c->d_gstat);
   if (c->d_dot) (void)hipFree(c->d_dot);
   if (c->d_topk) (void)hipFree(c->d_topk);
@@ -1171,6 +1298,7 @@ int frecsys_load_csr(frecsys_ctx* c, int32_t side, int64_t n_rows, const int64_t
   const int64_t nnz = row_ptr[n_rows] - row_ptr[0];
   if (row_ptr[0] != 0 || nnz < 0)
     return fail(c, FRECSYS_ERR_INVALID, "frecsys_load_csr: row_ptr must start at 0");
+  if (side < 2) c->pp_order_all[side].clear();  // the residual order of a sharded pp_step
   const int other = side == 1 ? 0 : 1;
   const int64_t n_other = c->n[other];
   for (int64_t i = 0; i < n_rows; ++i)
@@ -1425,14 +1553,16 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
                   hipStream_t aux = nullptr) {
   if (wide_dim(c->Dp)) {
     const size_t slot = wide_slot_floats(c->Dp);
-    const int64_t budget = (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (slot * sizeof(float)));
-    const int64_t batch = std::max<int64_t>(1, std::min<int64_t>(ap.n_rows, budget));
-    int rc = ensure(c, &c->wide_ws, &c->cap_wide_ws, (size_t)batch * slot);
+    const int64_t budget =
+        (int64_t)(ws_budget(c, c->cap_wide_ws * sizeof(float)) / (slot * sizeof(float)));
+    int64_t batch = std::max<int64_t>(1, std::min<int64_t>(ap.n_rows, budget));
+    int rc = ensure_batch(c, &c->wide_ws, &c->cap_wide_ws, slot, &batch);
     if (rc) return rc;
     if (can_split) {  // long histories of the first batch cut into slabs (a budget of their own)
       const size_t sf = wide_slab_floats(c->Dp);
       rc = plan_split(c, hs, batch, heff, &ap, wide_slab_rows(), sf,
-                      (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / (sf * sizeof(float))), s);
+                      (int64_t)(ws_budget(c, c->cap_slabs * sizeof(float)) / (sf * sizeof(float))),
+                      s, true);
       if (rc) return rc;
     }
     static const bool wprof = getenv("FRECSYS_DUAL_PROF") != nullptr;
@@ -1444,8 +1574,11 @@ int launch_dspace(frecsys_ctx* c, SolveArgs ap, const std::vector<int32_t>& hs,
     ap.prof = wprof ? w_prof : nullptr;
     char* xs = nullptr;
     if (c->wide_presplit && ap.n_rows > 0) {
-      rc = ensure(c, &c->wide_xs, &c->cap_wide_xs, wide_xsplit_bytes(c->Dp, ap.n_other));
+      // no room for the table: the register-staged SYRK (bit-identical)
+      bool oom = false;
+      rc = try_ensure(c, &c->wide_xs, &c->cap_wide_xs, wide_xsplit_bytes(c->Dp, ap.n_other), &oom);
       if (rc) return rc;
+      if (oom) ++c->ws_shrinks;
       xs = c->wide_xs;
     }
     const size_t k = ktimer_begin(c, pre + ".dspace", s);
@@ -1747,14 +1880,15 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
         // the wide bucket, 256 < h_eff <= 512, in batches of its workspace
         const int64_t hi = std::min(n_nonempty, first_le(32 * kDualMaxTiles));
         const size_t per = dual_wide_zs_bytes(c->Dp) + sizeof(float) * (dual_wide_slot_floats() + 512);
-        const int64_t nbat = std::max<int64_t>(
-            1, std::min<int64_t>(hi - lo, (int64_t)((size_t)c->wide_ws_mb * (1u << 20) / per)));
+        const size_t held = c->cap_dw_zs + sizeof(float) * (c->cap_dw_slots + c->cap_dw_z);
+        int64_t nbat = std::max<int64_t>(
+            1, std::min<int64_t>(hi - lo, (int64_t)(ws_budget(c, held) / per)));
         if (hi > lo) {
-          rc = ensure(c, &c->dw_zs, &c->cap_dw_zs, dual_wide_zs_bytes(c->Dp) * (size_t)nbat);
+          rc = ensure_batch(c, &c->dw_zs, &c->cap_dw_zs, dual_wide_zs_bytes(c->Dp), &nbat);
           if (rc) return rc;
-          rc = ensure(c, &c->dw_slots, &c->cap_dw_slots, dual_wide_slot_floats() * (size_t)nbat);
+          rc = ensure_batch(c, &c->dw_slots, &c->cap_dw_slots, dual_wide_slot_floats(), &nbat);
           if (rc) return rc;
-          rc = ensure(c, &c->dw_z, &c->cap_dw_z, (size_t)512 * nbat);
+          rc = ensure_batch(c, &c->dw_z, &c->cap_dw_z, (size_t)512, &nbat);
           if (rc) return rc;
         }
         for (int64_t b0 = lo; b0 < hi; b0 += nbat) {
@@ -2067,10 +2201,11 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
   // brings up to date for the other ranks' rows (pp_refresh_kernel, bitwise
   // the owner's update); EVAL rows are not sharded
   const bool sharded = side < 2 && c->world > 1;
+  const bool xchg = sharded && in_call_exchange(c);  // RCCL or the caller's transport
   int64_t lo = 0, hi = c->n[side];
   if (sharded) shard(c, side, &lo, &hi);
   const int bw = end - start;
-  if (sharded) {
+  if (sharded) {  // the block columns before the step: the refresh replays Delta from them
     int rc = ensure(c, &c->d_pp_old, &c->cap_pp_old,
                     (size_t)std::max<int64_t>(c->n[side], 1) * bw);
     if (rc) return rc;
@@ -2078,9 +2213,6 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
       HIP_TRY(c, hipMemcpy2DAsync(c->d_pp_old, sizeof(float) * bw, c->emb[side] + start,
                                   sizeof(float) * c->Dp, sizeof(float) * bw, c->n[side],
                                   hipMemcpyDeviceToDevice, c->stream));
-    c->pp_old_side = side;
-    c->pp_old_start = start;
-    c->pp_old_bw = bw;
   }
   std::vector<QueueRec> recs((size_t)(hi - lo));
   const std::vector<int64_t>& rp = side == 2 ? c->host_rp_eval : c->host_rp[side];
@@ -2116,21 +2248,27 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
   {
     ScopedTimer t(c, "pp_step");
     HIP_TRY(c, launch_pp_step(a, c->stream));
-    if (sharded && c->comm) {
+    if (sharded && !xchg) {  // the caller exchanges the rows, then frecsys_pp_sync
+      c->pp_old_side = side;
+      c->pp_old_start = start;
+      c->pp_old_bw = bw;
+    }
+    if (xchg) {
       // the rows of every rank, then the other ranks' prediction updates
-      rc = allgather_rows(c, c->emb[side], side, c->Dp);
+      rc = xchg_rows(c, c->emb[side], side, c->Dp);
       if (rc) return rc;
       HIP_TRY(c, launch_pp_refresh(a, c->rp[side], c->d_pp_old, c->n[side], lo, hi, c->stream));
-      c->pp_old_side = -1;
     }
     t.stop();
   }
-  if (sharded && c->comm)  // every rank takes the same NOT_SPD verdict
-    NCCL_TRY(c, ncclAllReduce(c->d_fail, c->d_fail, 1, ncclUint64, ncclMin, c->comm, c->stream));
+  if (xchg) {  // every rank takes the same NOT_SPD verdict
+    rc = xchg_min_u64(c, c->d_fail);
+    if (rc) return rc;
+  }
   std::vector<float> res(recs.size());
   unsigned long long f = none;
   HIP_TRY(c, hipMemcpyAsync(&f, c->d_fail, sizeof(f), hipMemcpyDeviceToHost, c->stream));
-  if (residual && !recs.empty())
+  if ((residual || xchg) && !recs.empty())
     HIP_TRY(c, hipMemcpyAsync(res.data(), c->d_resid, sizeof(float) * recs.size(),
                               hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -2139,19 +2277,61 @@ int frecsys_pp_step(frecsys_ctx* c, int32_t side, int32_t start, int32_t end,
     c->err_entity = (int64_t)(f - 1);
     return fail(c, FRECSYS_ERR_NOT_SPD, "pp_step: block matrix not SPD");
   }
-  if (residual) {
-    double s = 0.0;
-    for (float v : res) s += (double)v;  // zero rows (empty histories) stay 0
-    if (sharded && c->comm) {  // the sum over every rank's rows
-      rc = ensure(c, &c->d_dot, &c->cap_dot, 1);
-      if (rc) return rc;
-      HIP_TRY(c, hipMemcpyAsync(c->d_dot, &s, sizeof(double), hipMemcpyHostToDevice, c->stream));
-      NCCL_TRY(c, ncclAllReduce(c->d_dot, c->d_dot, 1, ncclFloat64, ncclSum, c->comm, c->stream));
-      HIP_TRY(c, hipMemcpyAsync(&s, c->d_dot, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-      HIP_TRY(c, hipStreamSynchronize(c->stream));
+  double s = 0.0;
+  if (xchg) {
+    // every rank's per-row residuals (all-gathered as a one-column table,
+    // whether or not this rank asked for the sum: the ranks' exchanges stay
+    // in step), summed in the single-rank queue order -- every row of the
+    // side by decreasing h: the world-1 sum bit for bit
+    const int64_t n = c->n[side];
+    std::vector<int32_t>& all = c->pp_order_all[side];
+    if ((int64_t)all.size() != n) {
+      all.resize((size_t)n);
+      for (int64_t i = 0; i < n; ++i) all[i] = (int32_t)i;
+      std::stable_sort(all.begin(), all.end(), [&](int32_t x, int32_t y) {
+        return rp[x + 1] - rp[x] > rp[y + 1] - rp[y];
+      });
     }
-    *residual = s;
+    std::vector<float> ent((size_t)std::max<int64_t>(n, 1), 0.0f);
+    for (size_t i = 0; i < recs.size(); ++i) ent[recs[i].entity] = res[i];
+    rc = ensure(c, &c->d_resid_e, &c->cap_resid_e, (size_t)std::max<int64_t>(n, 1));
+    if (rc) return rc;
+    if (n) HIP_TRY(c, hipMemcpyAsync(c->d_resid_e, ent.data(), sizeof(float) * n,
+                                     hipMemcpyHostToDevice, c->stream));
+    rc = xchg_rows(c, c->d_resid_e, side, 1);
+    if (rc) return rc;
+    if (n) HIP_TRY(c, hipMemcpyAsync(ent.data(), c->d_resid_e, sizeof(float) * n,
+                                     hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (int32_t e : all) s += (double)ent[e];
+  } else {
+    for (float v : res) s += (double)v;  // zero rows (empty histories) stay 0
   }
+  if (residual) *residual = s;
+  return FRECSYS_OK;
+}
+
+int frecsys_pp_get_predictions(frecsys_ctx* c, int32_t side, float* host) {
+  if (!c || (side != 0 && side != 2) || !host)
+    return fail(c, FRECSYS_ERR_INVALID, "pp_get_predictions: bad arguments");
+  const float* p = c->d_pred[side == 2 ? 1 : 0];
+  if (!p) return fail(c, FRECSYS_ERR_INVALID, "pp_get_predictions: no prediction vector");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int64_t nnz = c->nnz[side];
+  if (nnz)
+    HIP_TRY(c, hipMemcpyAsync(host, p, sizeof(float) * nnz, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FRECSYS_OK;
+}
+
+int frecsys_set_transport(frecsys_ctx* c, const frecsys_transport* t) {
+  if (!c) return FRECSYS_ERR_INVALID;
+  if (t && (!t->allgather_rows || !t->allreduce_min_u64))
+    return fail(c, FRECSYS_ERR_INVALID, "set_transport: every callback is required");
+  if (c->pp_old_side != -1)
+    return fail(c, FRECSYS_ERR_INVALID, "set_transport: pp_sync pending");
+  c->has_transport = t != nullptr;
+  c->transport = t ? *t : frecsys_transport{};
   return FRECSYS_OK;
 }
 
@@ -2237,6 +2417,26 @@ int frecsys_synchronize(frecsys_ctx* c) {
   return FRECSYS_OK;
 }
 
+int frecsys_release_workspaces(frecsys_ctx* c) {
+  if (!c) return FRECSYS_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream5));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  auto rel = [&](auto** p, size_t* cap) -> int {
+    if (*p) HIP_TRY(c, hipFree(*p));
+    *p = nullptr;
+    *cap = 0;
+    return FRECSYS_OK;
+  };
+  int rc = rel(&c->wide_ws, &c->cap_wide_ws);
+  if (!rc) rc = rel(&c->wide_xs, &c->cap_wide_xs);
+  if (!rc) rc = rel(&c->d_slabs, &c->cap_slabs);
+  if (!rc) rc = rel(&c->dw_zs, &c->cap_dw_zs);
+  if (!rc) rc = rel(&c->dw_slots, &c->cap_dw_slots);
+  if (!rc) rc = rel(&c->dw_z, &c->cap_dw_z);
+  return rc;
+}
+
 int frecsys_timing(const frecsys_ctx* c, const char* what, double* total_ms, int64_t* launches) {
   if (!c || !what) return FRECSYS_ERR_INVALID;
   auto it = c->timers.find(what);
@@ -2307,6 +2507,10 @@ int frecsys_counter(frecsys_ctx* c, const char* what, int64_t* value) {
   if (!c || !what || !value) return fail(c, FRECSYS_ERR_INVALID, "counter: bad arguments");
   if (!strcmp(what, "hspace_reruns")) {
     *value = c->hspace_reruns;
+    return FRECSYS_OK;
+  }
+  if (!strcmp(what, "ws_shrinks")) {
+    *value = c->ws_shrinks;
     return FRECSYS_OK;
   }
   if (!strcmp(what, "tagged_timeouts")) {

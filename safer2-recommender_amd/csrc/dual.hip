@@ -606,18 +606,25 @@ __device__ __forceinline__ void chol_solve_wave(float* tiles, float* bvec, float
   wave_sync();
 }
 
+// LDS per wave does not grow with Dp: the entity's l_k and D^-1/2 pass
+// through a 64-float window one slab at a time (loaded a slab ahead with the
+// rows), and c_j stays in its row's lane.  Staging the whole table row (2 Dp
+// floats) held the launch to 1 workgroup per CU at Dp = 1024 (one wave per
+// SIMD) and 2 at Dp = 256 / 512; now TH = 2 fits 3 (its register limit) and
+// TH = 1 fits 4 at every Dp.
 template <int TH, bool BF>
 struct WaveCfg {
   static constexpr int HP = 32 * TH;
   static constexpr int NT = TH * (TH + 1) / 2;
   static constexpr int ZS = (BF ? 48 : 32) * HP;
   static constexpr int REG = NT * 1024 > ZS ? NT * 1024 : ZS;
-  static constexpr int OFF_ID = REG, OFF_C = OFF_ID + HP, OFF_B = OFF_C + HP, OFF_X = OFF_B + HP;
+  static constexpr int OFF_ID = REG, OFF_B = OFF_ID + HP, OFF_X = OFF_B + HP;
   static constexpr int OFF_FLAG = OFF_X + HP;
-  static constexpr int OFF_T = OFF_FLAG + 4;  // l_k and D^-1/2 (table row), 2 * Dp
-  static constexpr int pw(int Dp) { return OFF_T + 2 * Dp; }  // floats per wave
+  static constexpr int OFF_T = OFF_FLAG + 4;  // the slab's l_k [32], then D^-1/2 [32]
+  static constexpr int pw(int) { return OFF_T + 64; }  // floats per wave
   static constexpr size_t bytes(int Dp) { return (size_t)4 * pw(Dp) * 4; }
   static_assert(TH <= 2, "one history row per lane");
+  static_assert(3 * ((bytes(0) + 511) / 512) * 512 <= 163840, "three workgroups per CU");
 };
 
 template <int TH, bool BF>
@@ -634,7 +641,6 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   float* zs = base;
   float* tiles = base;
   int* ids = reinterpret_cast<int*>(base + C::OFF_ID);
-  float* cvec = base + C::OFF_C;
   float* bvec = base + C::OFF_B;
   float* xvec = base + C::OFF_X;
   int* flag = reinterpret_cast<int*>(base + C::OFF_FLAG);
@@ -663,19 +669,15 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   }
   if (j < HP) {
     ids[j] = id;
-    cvec[j] = cj;
     bvec[j] = j < h ? cj : 0.0f;
   }
   if (lane == 0) flag[0] = 0;
-  // the entity's l_k and D^-1/2 into LDS: the recurrence then waits on LDS
-  // only (lgkmcnt), never behind the in-flight slab prefetch (vmcnt is in
-  // order)
+  // the slab's l_k (lanes 0-31) and D^-1/2 (lanes 32-63) of the entity's
+  // table row, loaded with the slab's rows and written to the wave's window
+  // when the slab starts: the recurrence then waits on LDS only (lgkmcnt)
   float* trow = base + C::OFF_T;
-  {
-    const int64_t pp = a.pos0 + pos;
-    for (int k = lane; k < 2 * Dp; k += 64)
-      trow[k] = a.table[blk_t(pp, k >= Dp, k >= Dp ? k - Dp : k, Dp)];
-  }
+  const int64_t tpp = a.pos0 + pos;
+  auto tload = [&](int c) { return a.table[blk_t(tpp, lane >> 5, 32 * c + lo, Dp)]; };
   const float* xrow = a.Xrot + (int64_t)(id < 0 ? 0 : id) * Dp;
 
   float4 yr[8], yn[8];
@@ -685,6 +687,7 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) dst[q] = *reinterpret_cast<const float4*>(xrow + 32 * c + 4 * q);
   };
+  float tn = tload(0);
   load(0, yn);
   wave_sync();
   f32x16 acc[NT];
@@ -696,7 +699,12 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
     // everything below runs on registers / LDS only
 #pragma unroll
     for (int q = 0; q < 8; ++q) yr[q] = yn[q];
-    if (c + 1 < NC) load(c + 1, yn);
+    trow[lane] = tn;  // the previous slab's window reads finished at its wave_sync
+    if (c + 1 < NC) {
+      tn = tload(c + 1);
+      load(c + 1, yn);
+    }
+    wave_sync();
     if (j < HP) {
       float z = carry;
       if constexpr (BF) {
@@ -708,9 +716,9 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
           for (int u = 0; u < 8; ++u) {
             const float4 y4 = yr[2 * gh + (u >> 2)];
             const float yv = (u & 3) == 0 ? y4.x : (u & 3) == 1 ? y4.y : (u & 3) == 2 ? y4.z : y4.w;
-            const int k = 32 * c + 8 * gh + u;
+            const int k = 8 * gh + u;
             z = yv - trow[k] * z;
-            v[u] = (cj * z) * trow[Dp + k];
+            v[u] = (cj * z) * trow[32 + k];
           }
           bf16x8 f[3];
           split3x8(v, f);
@@ -723,9 +731,9 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
           const float yv[4] = {yr[q].x, yr[q].y, yr[q].z, yr[q].w};
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const int kk = 4 * q + u, k = 32 * c + kk;
-            z = yv[u] - trow[k] * z;
-            zs[kk * HP + j] = (cj * z) * trow[Dp + k];
+            const int kk = 4 * q + u;
+            z = yv[u] - trow[kk] * z;
+            zs[kk * HP + j] = (cj * z) * trow[32 + kk];
           }
         }
       }
@@ -794,8 +802,8 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
         const int jj = j0 + u;
         wv[u] = 0.0f;
         rv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (jj < ntot) {
-          wv[u] = cvec[jj] * xvec[jj];
+        if (jj < ntot) {  // c_j from row jj's lane (jj wave-uniform)
+          wv[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cj), jj)) * xvec[jj];
           rv[u] = *reinterpret_cast<const float4*>(a.Xrot + (int64_t)ids[jj] * Dp + c4);
         }
       }

@@ -37,6 +37,8 @@
 // (tests/test_wide_syrk3_gpu.py).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 #include "wide.h"
@@ -59,41 +61,46 @@ constexpr int W3OFF_TAIL = W3OFF_IDS + W3IDS * kWideChunk * 4;
 constexpr int W3LDS = W3OFF_TAIL + W3NS * kWideChunk * 16;
 
 // ---- pre-split table ----
+// Grid-stride over the (n + 1) * Dp / 4 column quads: the grid is capped
+// (launch_wide_presplit), so any row count launches (a one-thread-per-quad
+// grid passes 2^32 work-items past ~16.7M rows at Dp = 1024).
 __global__ void __launch_bounds__(256)
     wide_presplit_kernel(const float* __restrict__ X, int64_t n, int Dp,
                          const float* __restrict__ nu, char* __restrict__ xs, int64_t rb) {
 #pragma clang fp contract(off)
   const int per_row = Dp >> 2;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t r = t / per_row;
-  const int c4 = (int)(t % per_row) * 4;
-  if (r > n) return;
-  char* row = xs + r * rb;
-  if (r == n) {  // the zero row
+  const int64_t total = (n + 1) * per_row;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += stride) {
+    const int64_t r = t / per_row;
+    const int c4 = (int)(t % per_row) * 4;
+    char* row = xs + r * rb;
+    if (r == n) {  // the zero row
 #pragma unroll
-    for (int p = 0; p < 3; ++p)
-      *reinterpret_cast<uint2*>(row + 2 * ((int64_t)p * Dp + c4)) = make_uint2(0u, 0u);
-    if (c4 == 0) *reinterpret_cast<float4*>(row + 6 * (int64_t)Dp) = make_float4(0.f, 0.f, 0.f, 0.f);
-    return;
-  }
-  float sa = 1.0f, bw = 1.0f;
-  if (nu) {  // rows pre-scaled by sqrt(nu); rhs weight nu / sqrt(nu) (safer2.h:190-192)
-    const float w = nu[r];
-    sa = sqrtf(w);
-    bw = sa > 0.0f ? w / sa : 0.0f;
-  }
-  const float4 x4 = *reinterpret_cast<const float4*>(X + r * Dp + c4);
-  const float xv[4] = {x4.x * sa, x4.y * sa, x4.z * sa, x4.w * sa};
-  __bf16 pc[3][4];
+      for (int p = 0; p < 3; ++p)
+        *reinterpret_cast<uint2*>(row + 2 * ((int64_t)p * Dp + c4)) = make_uint2(0u, 0u);
+      if (c4 == 0) *reinterpret_cast<float4*>(row + 6 * (int64_t)Dp) = make_float4(0.f, 0.f, 0.f, 0.f);
+      continue;
+    }
+    float sa = 1.0f, bw = 1.0f;
+    if (nu) {  // rows pre-scaled by sqrt(nu); rhs weight nu / sqrt(nu) (safer2.h:190-192)
+      const float w = nu[r];
+      sa = sqrtf(w);
+      bw = sa > 0.0f ? w / sa : 0.0f;
+    }
+    const float4 x4 = *reinterpret_cast<const float4*>(X + r * Dp + c4);
+    const float xv[4] = {x4.x * sa, x4.y * sa, x4.z * sa, x4.w * sa};
+    __bf16 pc[3][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) split3(xv[j], pc[0][j], pc[1][j], pc[2][j]);
+    for (int j = 0; j < 4; ++j) split3(xv[j], pc[0][j], pc[1][j], pc[2][j]);
 #pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    uint2 u;
-    __builtin_memcpy(&u, pc[p], 8);
-    *reinterpret_cast<uint2*>(row + 2 * ((int64_t)p * Dp + c4)) = u;
+    for (int p = 0; p < 3; ++p) {
+      uint2 u;
+      __builtin_memcpy(&u, pc[p], 8);
+      *reinterpret_cast<uint2*>(row + 2 * ((int64_t)p * Dp + c4)) = u;
+    }
+    if (c4 == 0) *reinterpret_cast<float4*>(row + 6 * (int64_t)Dp) = make_float4(bw, 0.f, 0.f, 0.f);
   }
-  if (c4 == 0) *reinterpret_cast<float4*>(row + 6 * (int64_t)Dp) = make_float4(bw, 0.f, 0.f, 0.f);
 }
 
 // ---- LDS-DMA and the waits the compiler does not see ----
@@ -634,7 +641,10 @@ hipError_t launch_wide_presplit(int Dp, const SolveArgs& a, char* xs, hipStream_
   if (!wide_dim(Dp) || !xs) return hipErrorInvalidValue;
   const int64_t threads = (a.n_other + 1) * (Dp / 4);
   const float* nu = is_v_kind(a.kind) ? a.other_weight : nullptr;
-  hipLaunchKernelGGL(wide_presplit_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s,
+  // 256 CUs x 8 workgroups x 32 quads each per pass: far past the chip's
+  // residency, and the grid-stride loop takes any row count
+  const int64_t blocks = std::min<int64_t>((threads + 255) / 256, (int64_t)1 << 16);
+  hipLaunchKernelGGL(wide_presplit_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                      a.X, a.n_other, Dp, nu, xs, wide_xsplit_row_bytes(Dp));
   return hipGetLastError();
 }

@@ -40,7 +40,8 @@ EXPORTS = (
     "frecsys_history_space_max_h", "frecsys_comm_world", "frecsys_gram_groups",
     "frecsys_get_gram_groups", "frecsys_set_gram_groups", "frecsys_get_gramian",
     "frecsys_gram_plan", "frecsys_work", "frecsys_snapshot_residual", "frecsys_counter",
-    "frecsys_pp_sync",
+    "frecsys_pp_sync", "frecsys_release_workspaces", "frecsys_pp_get_predictions",
+    "frecsys_set_transport",
 )
 
 # Every symbol include/frecsys_model.h declares.
@@ -62,6 +63,18 @@ class _Config(ctypes.Structure):
     _fields_ = [("dim", ctypes.c_int32), ("device", ctypes.c_int32),
                 ("parity_quirks", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("n_users", ctypes.c_int64), ("n_items", ctypes.c_int64)]
+
+
+# frecsys_transport (include/frecsys_hip.h)
+_ROWS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32,
+                            ctypes.POINTER(ctypes.c_float), ctypes.c_int64, ctypes.c_int64,
+                            ctypes.c_int64, ctypes.c_int64)
+_MIN_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+
+
+class _Transport(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allgather_rows", _ROWS_FN),
+                ("allreduce_min_u64", _MIN_FN)]
 
 
 class _SolveParams(ctypes.Structure):
@@ -142,6 +155,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_snapshot_residual": (ctypes.c_int, [P, I32, P]),
         "frecsys_counter": (ctypes.c_int, [P, ctypes.c_char_p, P]),
         "frecsys_pp_sync": (ctypes.c_int, [P, I32]),
+        "frecsys_release_workspaces": (ctypes.c_int, [P]),
+        "frecsys_pp_get_predictions": (ctypes.c_int, [P, I32, P]),
+        "frecsys_set_transport": (ctypes.c_int, [P, P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -342,10 +358,15 @@ class Context:
         return float(sq.value)
 
     def counter(self, what: str) -> int:
-        """Cumulative event counter: "hspace_reruns" or "tagged_timeouts"."""
+        """Cumulative event counter: "hspace_reruns", "tagged_timeouts" or
+        "ws_shrinks"."""
         v = ctypes.c_int64()
         self._check(self.lib.frecsys_counter(self.h, what.encode(), ctypes.byref(v)))
         return int(v.value)
+
+    def release_workspaces(self) -> None:
+        """Free the wide-dim workspaces (resized at the next solve)."""
+        self._check(self.lib.frecsys_release_workspaces(self.h))
 
     # -- compute --
     def gramian(self, side: int, weights: Optional[np.ndarray] = None,
@@ -427,6 +448,45 @@ class Context:
 
     def pp_predict(self, side: int):
         self._check(self.lib.frecsys_pp_predict(self.h, side))
+
+    def pp_predictions(self, side: int, nnz: int) -> np.ndarray:
+        """The prediction vector (frecsys_pp_get_predictions), nnz floats."""
+        out = np.empty(max(nnz, 1), np.float32)
+        self._check(self.lib.frecsys_pp_get_predictions(self.h, side, _ptr(out)))
+        return out[:nnz]
+
+    def set_transport(self, allgather_rows, allreduce_min_u64):
+        """Exchange callbacks of external-exchange mode (frecsys_set_transport):
+        allgather_rows(side, rows, lo, hi) fills every rank's rows of the
+        (n_rows, ld) float32 array in place (rows [lo, hi) are this rank's);
+        allreduce_min_u64(value) -> the minimum over ranks.  None clears."""
+        if allgather_rows is None:
+            self._transport = None
+            self._check(self.lib.frecsys_set_transport(self.h, None))
+            return
+
+        def rows_cb(user, side, ptr, n, ld, lo, hi):
+            try:
+                arr = np.ctypeslib.as_array(ptr, shape=(max(n, 1) * ld,))[:n * ld].reshape(n, ld)
+                allgather_rows(int(side), arr, int(lo), int(hi))
+                return 0
+            except Exception:  # noqa: BLE001 -- reported to the library as a failed exchange
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        def min_cb(user, vp):
+            try:
+                vp[0] = int(allreduce_min_u64(int(vp[0])))
+                return 0
+            except Exception:  # noqa: BLE001
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        t = _Transport(None, _ROWS_FN(rows_cb), _MIN_FN(min_cb))
+        self._transport = t  # the callbacks live as long as the context uses them
+        self._check(self.lib.frecsys_set_transport(self.h, ctypes.byref(t)))
 
     def pp_step(self, side: int, start: int, end: int, reg: float, w: float,
                 reg_exp: float = 1.0, kind: int = 0, alpha: float = 0.0, entity_weight=None,

@@ -17,10 +17,14 @@ def _run(args, **env_over):
                           capture_output=True, text=True, timeout=120)
 
 
+def _plan(r):
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def test_gpus_n_launches_n_ranks():
     r = _run(["--gpus", "4", "--steps", "3", "--print-launch"])
-    assert r.returncode == 0, r.stderr
-    cmd = json.loads(r.stdout.strip().splitlines()[-1])
+    cmd = _plan(r)["launch"]
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
     assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
     assert "--master-addr=127.0.0.1" in cmd
@@ -30,8 +34,7 @@ def test_gpus_n_launches_n_ranks():
 
 def test_torchrun_env_is_used_as_is():
     r = _run(["--gpus", "2", "--print-launch"], WORLD_SIZE="2", RANK="1", LOCAL_RANK="1")
-    assert r.returncode == 0, r.stderr
-    assert json.loads(r.stdout.strip().splitlines()[-1]) is None  # no second launch
+    assert _plan(r)["launch"] is None  # no second launch
 
 
 def test_world_size_mismatch_refused():
@@ -47,12 +50,21 @@ def test_frecsys_env_refused():
     assert r.returncode != 0 and "refusing" in r.stderr
 
 
-def test_default_extras_config5_at_one_gpu_only():
+def test_default_extras_every_config_at_every_n():
+    """BASELINE configs[3] and [4] are defined on 8 GPUs: the driver's N = 8
+    run measures configs 3, 4 and 5 beside the headline."""
     import bench
-    one = bench.default_extras(1).split(",")
-    many = bench.default_extras(8).split(",")
-    assert "safer2_2m500k_d1024" in one and "safer2_2m500k_d1024" not in many
-    assert set(many) == {"safer2_ml20m_d256", "ials_msd_d512"}
+    for n in (1, 2, 4, 8):
+        assert bench.default_extras(n).split(",") == ["safer2_ml20m_d256", "ials_msd_d512",
+                                                      "safer2_2m500k_d1024"]
     assert bench.WORKLOADS["safer2_2m500k_d1024"]["max_extra_steps"] == 2
+    for n in (1, 8):
+        plan = _plan(_run(["--gpus", str(n), "--print-launch"]))
+        assert plan["n_gpus"] == n and plan["workload"] == "ials_ml20m_d256"
+        assert plan["extras"] == ["safer2_ml20m_d256", "ials_msd_d512", "safer2_2m500k_d1024"]
+        assert plan["cpu_baseline"] == (n == 1)  # the CPU baseline stays at N = 1
+        assert (plan["launch"] is None) == (n == 1)
+        if n == 8:
+            assert "--nproc-per-node=8" in plan["launch"]
     # every default extra is a BASELINE config the bench knows
-    assert all(w in bench.WORKLOADS for w in one)
+    assert all(w in bench.WORKLOADS for w in bench.DEFAULT_EXTRAS)

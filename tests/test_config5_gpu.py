@@ -1,13 +1,15 @@
 """BASELINE configs[4] at its real size on one GPU: SAFER2, d = 1024, the
 2M x 500K synthetic set with 1e8 interactions (README.md:100 flags,
-use_snr 0), the default 4 GB wide workspace.
+use_snr 0), the default wide workspace budget (FRECSYS_WIDE_WS_MB unset:
+16 GB per workspace, capped by the device's free memory, capi.hip).
 
 The product's C++ model (libfrecsys_model.so) runs Initialize() and one
 Train() epoch (safer2.h:266-334, 819-838): ComputeUserWeights, StepU over 2M
-users (history-space buckets + the wide d-space batches of the 32,920 users
-with h > 256), StepV over 500K items (the omega-weighted Gramian of 2M user
-rows, the basis of it, 37,938 wide d-space items incl. the split slabs of the
-head items up to 581K rows, the tail quirk), V^T V, ComputeUserLoss, xi.
+users (history-space buckets, the history-space wide bucket of the users with
+256 < h <= 512 and the wide d-space batches of the longer ones), StepV over
+500K items (the omega-weighted Gramian of 2M user rows, the basis of it, the
+wide bucket, the wide d-space items incl. the split slabs of the head items
+up to 581K rows, the tail quirk), V^T V, ComputeUserLoss, xi.
 
 Each sampled row is then stepped from the GPU's own inputs (V0 and its
 Gramian after Initialize(), the omega the epoch used, U after the epoch and
@@ -161,6 +163,36 @@ def test_config5_item_halfstep_random(c5):
                     out=c5["V0"][rows].copy())
     assert rc == 0
     _check("config5_item_random", c5["V1"][rows], Vo, rows, ip)
+
+
+def _heff_v(h):
+    return np.where((h > 128) & (h % 128 != 0), h + 128 - h % 128, h)
+
+
+def test_config5_wide_bucket_rows(c5):
+    """Rows the history-space wide bucket solves at this size (256 < h_eff <=
+    512, on by default at Dp = 1024): 40 users (ProjectU, omega) and 40 items
+    (ProjectV, nu, item_reg_, the tail quirk's h_eff) by the oracle.  The
+    random samples above hold only a couple of them."""
+    up, uc, ip, ic = c5["up"], c5["uc"], c5["ip"], c5["ic"]
+    rng = np.random.default_rng(55)
+    hu = np.diff(up)
+    urows = np.sort(rng.choice(np.nonzero((hu > 256) & (hu <= 512))[0], 40, replace=False))
+    rp, cl = _sub_csr(up, uc, urows)
+    Uo, rc = O.step(rp, cl, c5["V0"], c5["GV0"], 1, FLAGS["l2_reg"], FLAGS["uobs_weight"],
+                    entity_weight=c5["omega"][urows], out=c5["U0"][urows].copy())
+    assert rc == 0
+    _check("config5_user_wide_bucket", c5["U1"][urows], Uo, urows, up)
+    he = _heff_v(np.diff(ip))
+    irows = np.sort(rng.choice(np.nonzero((he > 256) & (he <= 512))[0], 40, replace=False))
+    reg_rows = _item_reg_ref(ip, ic, up, irows)
+    nu_w = (c5["omega"] / hu.astype(np.float32)).astype(np.float32)
+    rp, cl = _sub_csr(ip, ic, irows)
+    Vo, rc = O.step(rp, cl, c5["U1"], c5["GU1"], 2, FLAGS["l2_reg"], FLAGS["uobs_weight"],
+                    alpha=FLAGS["alpha"], entity_reg=reg_rows, other_weight=nu_w,
+                    out=c5["V0"][irows].copy())
+    assert rc == 0
+    _check("config5_item_wide_bucket", c5["V1"][irows], Vo, irows, ip)
 
 
 def test_config5_item_halfstep_longest(c5):

@@ -4,7 +4,10 @@ Cholesky) against the d-space solve of the same entities (FRECSYS_DUAL=0)
 and the oracle, every row at the 1e-4 bar (the same bar as test_dual_gpu.py):
 iALS on both sides (tridiagonal basis, and the Cholesky basis of
 l2_reg_exp = 0), ProjectU with entity weights, ProjectV with and without
-the tail quirk (h_eff up to 512 includes the quirk rows).
+the tail quirk (h_eff up to 512 includes the quirk rows).  At Dp = 1024
+(d = 1000, 1024: config 5's dims, SAFER2 = the weighted kinds) the bucket is on
+by default, so those cases run with no FRECSYS_* override at all; at Dp = 512
+the threshold is raised to 512 to reach it.  Margins go to parity_report.jsonl.
 """
 import numpy as np
 import pytest
@@ -45,8 +48,12 @@ def _heff(h, quirk):
 
 
 def _run(monkeypatch, data, dim, side, kind, wide, quirk=True, reg_exp=1.0):
-    monkeypatch.setenv("FRECSYS_DUAL", "1" if wide else "0")
-    monkeypatch.setenv("FRECSYS_DUAL_MAX_H", "512")
+    monkeypatch.delenv("FRECSYS_DUAL", raising=False)
+    monkeypatch.delenv("FRECSYS_DUAL_MAX_H", raising=False)
+    if not wide:
+        monkeypatch.setenv("FRECSYS_DUAL", "0")  # the d-space reference run
+    elif fh.padded_dim(dim) < 1024:
+        monkeypatch.setenv("FRECSYS_DUAL_MAX_H", "512")  # default 256 at Dp = 512
     nu, ni, up, uc, ip, ic = data
     ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic, quirks=quirk)
     om = _weights(nu)
@@ -97,6 +104,10 @@ def _check(monkeypatch, data, dim, side, kind, okind, quirk=True, reg_exp=1.0):
     ew, ed = rel_rows(Xw, Xo), rel_rows(Xd, Xo)
     print(f"side {side} dim {dim} kind {kind}: wide bucket {ew[wide].max():.2e} "
           f"(all rows {ew.max():.2e}), d-space {ed[wide].max():.2e}")
+    from test_models_gpu import report
+    report(test="wide_bucket", side=int(side), dim=dim, kind=kind, quirk=bool(quirk),
+           reg_exp=reg_exp, wide_rows=int(wide.sum()), max_wide_bucket=float(ew[wide].max()),
+           max_all=float(ew.max()), max_dspace=float(ed.max()), margin=TOL_ROW / float(ew.max()))
     assert ew.max() < TOL_ROW, (ew[wide].max(), ew.max())
     assert ed.max() < TOL_ROW
 
@@ -113,10 +124,15 @@ def test_wide_bucket_ials_chol_basis(monkeypatch, mid_data):
     _check(monkeypatch, mid_data, 512, fh.SIDE_USER, fh.KIND_IALS, 0, reg_exp=0.0)
 
 
-def test_wide_bucket_weighted_u(monkeypatch, mid_data):
-    _check(monkeypatch, mid_data, 512, fh.SIDE_USER, fh.KIND_WEIGHTED_U, 1)
+@pytest.mark.parametrize("dim", [512, 1000, 1024])
+def test_wide_bucket_weighted_u(monkeypatch, mid_data, dim):
+    # ProjectU (omega) -- config 5's user side at d = 1024
+    _check(monkeypatch, mid_data, dim, fh.SIDE_USER, fh.KIND_WEIGHTED_U, 1)
 
 
+@pytest.mark.parametrize("dim", [512, 1000, 1024])
 @pytest.mark.parametrize("quirk", [True, False])
-def test_wide_bucket_weighted_v(monkeypatch, mid_data, quirk):
-    _check(monkeypatch, mid_data, 512, fh.SIDE_ITEM, fh.KIND_WEIGHTED_V, 2, quirk=quirk)
+def test_wide_bucket_weighted_v(monkeypatch, mid_data, quirk, dim):
+    # ProjectV (nu, item_reg), with and without the tail quirk -- config 5's
+    # item side at d = 1024
+    _check(monkeypatch, mid_data, dim, fh.SIDE_ITEM, fh.KIND_WEIGHTED_V, 2, quirk=quirk)
