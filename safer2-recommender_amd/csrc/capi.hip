@@ -1799,7 +1799,8 @@ int solve_side_impl(frecsys_ctx* c, int32_t side, const frecsys_solve_params* p,
       if (n_dspace > 0) HIP_TRY(c, hipEventRecord(c->ev_fork, c->stream));
       // one M = mu*G + lam*I for every entity (iALS with l2_reg_exp = 0, or
       // lambda = reg: ials.h:310-315): the Cholesky basis, no tridiagonal
-      // reduction, no per-entity LDL
+      // reduction, no per-entity LDL -- at every Dp the history space runs
+      // at (64..256, 512, 1024: chol_basis_kernel<T>, launch_chol_basis)
       int bmode = 0;
       float bmu = 0.f, blam = 0.f;
       if (c->chol_basis_on && kind == FRECSYS_KIND_IALS &&

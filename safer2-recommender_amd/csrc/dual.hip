@@ -520,8 +520,9 @@ __global__ void __launch_bounds__((DualCfg<TH, BF>::NTHR))
 // ---------------------------------------------------------------------
 // Short histories (h_eff <= 64): one wave per entity, four independent
 // entities per workgroup, no workgroup barrier anywhere.  Lane j owns
-// history row j: it loads the row's 32-column slab straight into registers
-// (one slab ahead), runs the bidiagonal recurrence with l_k and D^-1/2 as
+// history row j: the wave fetches the rows' 32-column slab (coalesced, one
+// slab ahead) and hands lane j its row through LDS, lane j runs the
+// bidiagonal recurrence with l_k and D^-1/2 as
 // wave-uniform scalars from the entity's table row, and writes the scaled
 // values k-major to its wave's LDS slab; the same wave then accumulates
 // the S tiles with MFMA, factors S (chol_solve_wave) and forms Y^T (c.*z)
@@ -617,7 +618,8 @@ struct WaveCfg {
   static constexpr int HP = 32 * TH;
   static constexpr int NT = TH * (TH + 1) / 2;
   static constexpr int ZS = (BF ? 48 : 32) * HP;
-  static constexpr int REG = NT * 1024 > ZS ? NT * 1024 : ZS;
+  static constexpr int REG0 = NT * 1024 > ZS ? NT * 1024 : ZS;
+  static constexpr int REG = REG0 > HP * 36 ? REG0 : HP * 36;  // + the coalesced slab staging
   static constexpr int OFF_ID = REG, OFF_B = OFF_ID + HP, OFF_X = OFF_B + HP;
   static constexpr int OFF_FLAG = OFF_X + HP;
   static constexpr int OFF_T = OFF_FLAG + 4;  // the slab's l_k [32], then D^-1/2 [32]
@@ -681,11 +683,36 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   const float* xrow = a.Xrot + (int64_t)(id < 0 ? 0 : id) * Dp;
 
   float4 yr[8], yn[8];
+#ifndef FRECSYS_WAVE_COAL
+#define FRECSYS_WAVE_COAL 1
+#endif
+  // COAL (default): the slab's rows are fetched 8 lanes per row (8 rows x
+  // 128 B per instruction, 8 cache lines) and turned to one row per lane
+  // through the wave's zs area (rows padded to 36 floats: conflict-free both
+  // ways), instead of each lane fetching its own row's 128 B (64 lines per
+  // instruction).  Bit-identical; config 5 1230 -> 1207 ms per epoch, MSD
+  // and ML-20M unchanged (profiles/r06/wave_coal/).
+  constexpr bool COAL = FRECSYS_WAVE_COAL != 0;
+  constexpr int NQ = COAL ? HP / 8 : 8;  // prefetch registers per lane
+  // COAL: row 8 q + lane / 8's offset (32-bit while rows x Dp < 2^32, as the
+  // wave's own rows: the wave kernels run at Dp <= 1024 on tables < 4G floats)
+  uint32_t coff[COAL ? NQ : 1];
+  if constexpr (COAL) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+      coff[q] = (uint32_t)max(ids[8 * q + (lane >> 3)], 0) * (uint32_t)Dp + 4u * (lane & 7);
+  }
   // unconditional loads (row 0 stands in for padding rows, whose c_j = 0):
   // no branches around the loads, so the prefetch stays in flight
   auto load = [&](int c, float4* dst) {
+    if constexpr (COAL) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) dst[q] = *reinterpret_cast<const float4*>(xrow + 32 * c + 4 * q);
+      for (int q = 0; q < NQ; ++q)
+        dst[q] = *reinterpret_cast<const float4*>(a.Xrot + (size_t)(coff[q] + 32u * c));
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) dst[q] = *reinterpret_cast<const float4*>(xrow + 32 * c + 4 * q);
+    }
   };
   float tn = tload(0);
   load(0, yn);
@@ -697,14 +724,32 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   for (int c = 0; c < NC; ++c) {
     // slab c arrives (the one wait per slab), slab c+1 goes in flight, and
     // everything below runs on registers / LDS only
+    if constexpr (COAL) {
+      // the previous slab's zs reads finished at its closing wave_sync
 #pragma unroll
-    for (int q = 0; q < 8; ++q) yr[q] = yn[q];
+      for (int q = 0; q < NQ; ++q)  // (component stores: a float4 struct copy stays in scratch)
+        *reinterpret_cast<f32x4v*>(zs + (8 * q + (lane >> 3)) * 36 + 4 * (lane & 7)) =
+            f32x4v{yn[q].x, yn[q].y, yn[q].z, yn[q].w};
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) yr[q] = yn[q];
+    }
     trow[lane] = tn;  // the previous slab's window reads finished at its wave_sync
     if (c + 1 < NC) {
       tn = tload(c + 1);
       load(c + 1, yn);
     }
     wave_sync();
+    if constexpr (COAL) {
+      if (j < HP) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const f32x4v t = *reinterpret_cast<const f32x4v*>(zs + j * 36 + 4 * q);
+          yr[q] = make_float4(t[0], t[1], t[2], t[3]);
+        }
+      }
+      wave_sync();  // the recurrence overwrites zs with the pieces
+    }
     if (j < HP) {
       float z = carry;
       if constexpr (BF) {
@@ -790,15 +835,16 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
   chol_solve_wave<TH>(tiles, bvec, xvec, flag, lane, a.debug_skip);
 
   // v = Y^T (c.*z): lane owns columns 4*lane + 256*cg .. +3
+  constexpr int YZ = 8;  // row loads in flight (16 measured the same)
   for (int cg = 0; 256 * cg < Dp; ++cg) {
   const int c4 = 4 * lane + 256 * cg;
   float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c4 < Dp && !FRECSYS_SKIP(a.debug_skip, 64)) {
-    for (int j0 = 0; j0 < ntot; j0 += 8) {
-      float4 rv[8];
-      float wv[8];
+    for (int j0 = 0; j0 < ntot; j0 += YZ) {
+      float4 rv[YZ];
+      float wv[YZ];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < YZ; ++u) {
         const int jj = j0 + u;
         wv[u] = 0.0f;
         rv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -808,7 +854,7 @@ __global__ void __launch_bounds__(256) dual_wave_kernel(DualArgs a) {
         }
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < YZ; ++u) {
         v4.x += wv[u] * rv[u].x;
         v4.y += wv[u] * rv[u].y;
         v4.z += wv[u] * rv[u].z;

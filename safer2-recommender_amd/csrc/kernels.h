@@ -212,7 +212,9 @@ size_t basis_split_bytes(int Dp);
 hipError_t launch_split_basis(const float* Q, int Dp, int trans, void* out, hipStream_t s);
 // Cholesky basis of M = mu*G + lam*I (one workgroup): XT = L^-T (Dp x Dp,
 // row-major, upper triangular) with M = L L^T; status[0] = 1, or 0 on a
-// non-positive pivot.  work: chol_basis_work_floats(Dp).  Dp = 64..256, 512.
+// non-positive pivot.  work: chol_basis_work_floats(Dp).  Dp = 64..256, 512,
+// 1024 (T = 32: 7 staging tiles beside the 31-tile panel in the 160 KB of
+// LDS, spectral.hip chol_basis_stage_tiles).
 size_t chol_basis_work_floats(int Dp);
 hipError_t launch_chol_basis(const float* G, int Dp, float mu, float lam, float* work, float* XT,
                              float* status, hipStream_t s);
