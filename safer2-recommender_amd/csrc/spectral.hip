@@ -17,6 +17,7 @@
 //                  partials of the wide user loss.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "chol.h"
@@ -553,10 +554,10 @@ __global__ void __launch_bounds__(256)
     for (int q = 0; q < 16; ++q) {
       const int64_t p = base + 32 * R + acc_row(q, hi);
       float sv = 0.0f;
-      if (p < n) {
-#pragma unroll
-        for (int j = 0; j < CW; ++j)
-          if (C0 + j < NCT) sv += acc[j][q] * X[(r0 + p) * DP + 32 * (C0 + j) + lo];
+      if (p < n) {  // explicit fma: the same rounding in rotate_lds_kernel
+        const float* xp = X + (r0 + p) * DP + 32 * C0 + lo;
+        if (CW == 2 && C0 + 1 < NCT) sv = __builtin_fmaf(acc[CW - 1][q], xp[32], acc[0][q] * xp[0]);
+        else if (C0 < NCT) sv = acc[0][q] * xp[0];
       }
 #pragma unroll
       for (int o = 16; o > 0; o >>= 1) sv += __shfl_xor(sv, o);  // the 32 columns of a half
@@ -844,6 +845,199 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// ---- Rotation GEMM from LDS-DMA stages (Dp = 256, 512, 1024) ----
+// Y = X B for B given by its split image (Q, Q^T, or G for the u^T G u
+// partials), the work of rotate_rt_kernel / rotate_kernel on a larger block:
+// one workgroup of 8 waves per 256 x 256 block of Y; every k16 step, X's 256
+// rows (fp32, 16 KB) and B's 24 granule-KB of the block's 8 column tiles
+// arrive by LDS-DMA in a 3-stage ring two steps ahead (no VGPR staging, one
+// barrier per step).  Wave w takes row tiles 2 (w >> 1), +1 x column tiles
+// 4 (w & 1) .. +3: each B fragment set feeds two row tiles, each split A
+// fragment four column tiles.  Per block and step 40 KB of intake for 384
+// MFMAs, against 8 KB per wave and 24 MFMAs in rotate_rt_kernel (whose B
+// fragments every wave fetched from L2 / MALL).  X rows land row-major with
+// their 16-B quads XOR-swizzled by row / 4 (set on the DMA's source address,
+// conflict-free b128 reads); position-blocked X (XB: the back rotation's
+// out_rot) lands k-major, one k per DMA.  Every output element sees the same
+// products in the same k order as the older kernels (mfma_x6 of split3x8(X)
+// and the image's pieces), and the u^T G u partials the same sums per
+// 128-column half: bit-identical.
+constexpr int RL_ROWS = 256, RL_STG = 3;
+constexpr int RL_A = RL_ROWS * 16 * 4;  // 16 KB: 256 rows x 16 k, fp32
+constexpr int RL_B = 8 * 3 * 1024;      // 24 KB: 8 column tiles x 3 pieces x 64 granules
+constexpr int RL_STAGE = RL_A + RL_B;
+constexpr size_t RL_LDS = (size_t)RL_STG * RL_STAGE;  // 120 KB: one workgroup per CU
+
+template <int DP, bool XB, bool QUAD>
+__global__ void __launch_bounds__(512)
+    rotate_lds_kernel(const float* __restrict__ X, const QueueRec* __restrict__ rows, int64_t r0,
+                      int64_t n, const bf16x8* __restrict__ Bs, float* __restrict__ Y, int ncb,
+                      float* __restrict__ qpart) {
+  constexpr int NCT = DP / 32, NS = DP / 16;
+  static_assert(DP % 256 == 0, "256-column blocks");
+  extern __shared__ __attribute__((aligned(16))) char rl_lds[];
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // slot b -> XCD b % 8; the ncb column blocks of a row block on one XCD
+  const int64_t bid = blockIdx.x, sx = bid >> 3;
+  const int cb = (int)(sx % ncb);
+  const int64_t base = ((sx / ncb) * 8 + (bid & 7)) * RL_ROWS;
+  if (base >= n) return;  // the whole workgroup
+  const int C0 = 8 * cb;  // the block's first column tile
+  const unsigned ring = lds_addr(rl_lds);
+  const char* lds = rl_lds;
+  (void)tid;
+
+  // this wave's two A DMAs per step: d = 2 wave + i
+  const float* asrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int d = 2 * wave + i;
+    if constexpr (XB) {  // k-row d of the step: positions base + 4 lane .. +3
+      const int64_t npos = (n + 63) / 64 * 64;  // out_rot's allocated positions
+      int64_t p4 = base + 4 * lane;
+      if (p4 >= npos) p4 = 0;
+      asrc[i] = X + (((p4 >> 6) * DP + d) << 6) + (p4 & 63);
+    } else {  // rows 16 d + lane / 4, quad lane & 3 of the swizzled row
+      const int rr = 16 * d + (lane >> 2);
+      const int64_t p = base + rr < n ? base + rr : base;
+      const int64_t id = rows ? (int64_t)rows[p].entity : r0 + p;
+      const int lq = (lane & 3) ^ ((rr >> 2) & 3);
+      asrc[i] = X + id * DP + 4 * lq;
+    }
+  }
+  const bf16x8* bsrc = Bs + (int64_t)C0 * 3 * 64 + lane;
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const unsigned st = ring + (unsigned)((s % RL_STG) * RL_STAGE);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      glds16(asrc[i] + (XB ? (int64_t)s * 16 * 64 : (int64_t)s * 16),
+             st + (unsigned)((2 * wave + i) * 1024));
+    const bf16x8* bs = bsrc + (int64_t)s * NCT * 3 * 64;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int kb = 3 * wave + i;
+      glds16(bs + kb * 64, st + (unsigned)(RL_A + kb * 1024));
+    }
+  };
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[t][c] = f32x16{0.f};
+  issue(0);
+  if (NS > 1) issue(1);
+  const int rbase = 64 * (wave >> 1), cw = 4 * (wave & 1);
+#pragma unroll 1
+  for (int s = 0; s < NS; ++s) {
+    vm_wait(s + 1 < NS ? 5 : 0);  // this wave's DMAs of stage s (not s + 1's)
+    w3_barrier();                 // every wave's stage s landed; stage s - 1 read
+    if (s + 2 < NS) issue(s + 2);  // into the slot of stage s - 1
+    const char* st = lds + (s % RL_STG) * RL_STAGE;
+    bf16x8 af[2][3];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int r = rbase + 32 * t + lo;
+      float v[8];
+      if constexpr (XB) {
+        const float* a = reinterpret_cast<const float*>(st);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = a[(8 * hi + j) * RL_ROWS + r];
+      } else {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const f32x4v x4 = *reinterpret_cast<const f32x4v*>(
+              st + r * 64 + 16 * ((2 * hi + g) ^ ((r >> 2) & 3)));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[4 * g + j] = x4[j];
+        }
+      }
+      split3x8(v, af[t]);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      bf16x8 bf[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bf[p] = *reinterpret_cast<const bf16x8*>(st + RL_A + (((cw + c) * 3 + p) * 64 + lane) * 16);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t][c] = mfma_x6(af[t], bf, acc[t][c]);
+    }
+  }
+  if constexpr (QUAD) {
+    // u^T G u partials: per 128-column half (column tiles cw .. cw + 3 =
+    // rotate_kernel's block 2 cb + (w & 1)) the row dots of its two 64-column
+    // wave halves, each reduced over the lanes, then added in that order
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t p = base + rbase + 32 * t + acc_row(q, hi);
+        float sh[2];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          float sv = 0.0f;
+          if (p < n) {  // as rotate_kernel's pair of column tiles
+            const float* xp = X + (r0 + p) * DP + 32 * (C0 + cw + 2 * hh) + lo;
+            sv = __builtin_fmaf(acc[t][2 * hh + 1][q], xp[32], acc[t][2 * hh][q] * xp[0]);
+          }
+#pragma unroll
+          for (int o = 16; o > 0; o >>= 1) sv += __shfl_xor(sv, o);
+          sh[hh] = sv;
+        }
+        if (lo == 0 && p < n) qpart[(int64_t)(2 * cb + (wave & 1)) * n + p] = sh[0] + sh[1];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int col = 32 * (C0 + cw + c) + lo;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t p = base + rbase + 32 * t + acc_row(q, hi);
+        if (p < n) {
+          const int64_t id = rows ? (int64_t)rows[p].entity : r0 + p;
+          Y[id * DP + col] = acc[t][c][q];
+        }
+      }
+    }
+}
+
+// FRECSYS_ROT_LDS=0: the register-fed rotation kernels only (A/B, bitwise
+// tests; read at every launch)
+#ifndef FRECSYS_ROT_LDS_DEFAULT
+#define FRECSYS_ROT_LDS_DEFAULT 1
+#endif
+bool rotate_lds_on() {
+  const char* v = getenv("FRECSYS_ROT_LDS");
+  return v ? atoi(v) != 0 : FRECSYS_ROT_LDS_DEFAULT != 0;
+}
+
+// rows the LDS kernel takes a launch from: fewer leave most CUs idle (one
+// 256-row block per CU), and the register-fed kernels spread them wider
+constexpr int64_t kRotLdsMinRows = 16384;
+
+template <int DP, bool XB, bool QUAD>
+hipError_t launch_rotate_lds_t(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
+                               const bf16x8* Bs, float* Y, float* qpart, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t err = hipFuncSetAttribute((const void*)rotate_lds_kernel<DP, XB, QUAD>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)RL_LDS);
+    if (err != hipSuccess) return err;
+    attr = true;
+  }
+  const int ncb = DP / 256;
+  const int64_t units = (n + RL_ROWS - 1) / RL_ROWS;
+  const unsigned grid = (unsigned)(((units + 7) / 8) * 8 * ncb);
+  hipLaunchKernelGGL((rotate_lds_kernel<DP, XB, QUAD>), dim3(grid), dim3(512), RL_LDS, s, X, rows,
+                     r0, n, Bs, Y, ncb, qpart);
+  return hipGetLastError();
+}
+
 // rotate_rt_kernel with 2 row tiles per wave and P = 2 k-steps of loads in
 // flight: 1.95 vs 2.20 ms (rotate_kernel) for the 471,355 x 512 rotation,
 // 0.138 vs 0.141 ms for 116,677 x 256, bit-identical; RT = 1 and P = 4
@@ -865,6 +1059,13 @@ template <int DP>
 hipError_t launch_rotate_t(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
                            const bf16x8* Bs, float* Y, hipStream_t s, int xb,
                            float* qpart = nullptr) {
+  if constexpr (DP % 256 == 0) {
+    if (rotate_lds_on() && n >= kRotLdsMinRows) {
+      if (qpart) return launch_rotate_lds_t<DP, false, true>(X, nullptr, r0, n, Bs, nullptr, qpart, s);
+      if (xb) return launch_rotate_lds_t<DP, true, false>(X, rows, r0, n, Bs, Y, nullptr, s);
+      return launch_rotate_lds_t<DP, false, false>(X, rows, r0, n, Bs, Y, nullptr, s);
+    }
+  }
   constexpr int CBc = (DP % 128 == 0) ? 4 : 2;
   const int ncbc = (DP / 32 + CBc - 1) / CBc;
   if (!qpart) {
