@@ -36,6 +36,9 @@
 //     Y^T (c.*z) re-reads the (cache-resident) rows with float4 loads.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <type_traits>
+
 #include "chol.h"
 #include "common.h"
 #include "kernels.h"
@@ -1043,6 +1046,128 @@ __global__ void __launch_bounds__(256) dual_wide_s_kernel(const bf16x8* zs_all, 
     }
 }
 
+// S of the wide bucket from LDS-DMA stages: two workgroups (8 waves) per
+// entity -- the off-diagonal 256 x 256 block (rows 256..511 x columns 0..255,
+// 64 tiles, wave w: rows 2 (w >> 1), +1 x columns 4 (w & 1) .. +3) and the two
+// diagonal triangles (72 tiles, wave w: triangle w >> 2, its rows q and 7 - q,
+// q = w & 3: 9 tiles) -- each reading every k16 step's fragments of all 16
+// row tiles (48 KB: 16 tiles x 3 pieces x 1 KB, the z kernel's fragment
+// layout) once into a 3-stage ring two steps ahead, instead of every wave of
+// dual_wide_s_kernel's 10 workgroups loading its own 12 KB from L2 (4 waves x
+// 12 KB for 24 MFMAs each: L2-bound, MFMA busy 0.29).  The tiles holding rows
+// (I < te) get the same products in the same k order as dual_wide_s_kernel
+// (bit-identical); the others are written as identity tiles (never read:
+// the Cholesky factors the te live tiles only).
+constexpr int WS_STG = 3, WS_STAGE = 16 * 3 * 1024;  // 48 KB
+constexpr size_t WS_LDS = (size_t)WS_STG * WS_STAGE;  // 144 KB: one workgroup per CU
+
+template <int ROLE>
+__global__ void __launch_bounds__(512) dual_wide_s_lds_kernel(const bf16x8* zs_all, int Dp,
+                                                              const QueueRec* order, int quirk_v,
+                                                              float* slots, int64_t slot_floats,
+                                                              int64_t n) {
+  extern __shared__ __attribute__((aligned(16))) char ws_lds[];
+  const int tid = threadIdx.x, lane = tid & 63, lo = lane & 31, hi = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // one launch per role (ROLE 0: the off-diagonal block, 1: the triangles)
+  constexpr int role = ROLE;
+  const int64_t b = blockIdx.x;
+  if (b >= n) return;
+  (void)tid;
+  float* slot = slots + b * slot_floats;
+  const QueueRec rec = order[b];
+  int64_t extra = 0;
+  if (quirk_v && rec.h > 128 && (rec.h % 128) != 0) extra = 128 - (rec.h % 128);
+  const int te = (int)((rec.h + extra + 31) / 32);  // tiles holding rows
+  const bf16x8* zs = zs_all + b * (Dp / 16) * 3 * 2 * kWideHP;
+  const unsigned ring = lds_addr(ws_lds);
+  const int NS = Dp / 16;
+  // this wave's 6 fragment DMAs per step: f = 6 w + i -> (tile f / 3, piece f % 3)
+  auto issue = [&](int kb) __attribute__((always_inline)) {
+    const unsigned st = ring + (unsigned)((kb % WS_STG) * WS_STAGE);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int f = 6 * wave + i, t = f / 3, p = f % 3;
+      glds16(zs + wz_gran(kb, p, hi, 32 * t + lo), st + (unsigned)(f * 1024));
+    }
+  };
+  // tile coordinates of accumulator slot m (global 32-row tiles)
+  auto tile_of = [&](int m, int& I, int& J) __attribute__((always_inline)) {
+    if constexpr (role == 0) {
+      I = 8 + 2 * (wave >> 1) + (m >> 2);
+      J = 4 * (wave & 1) + (m & 3);
+    } else {
+      const int tr = wave >> 2, q = wave & 3;
+      if (m <= 7 - q) {
+        I = 8 * tr + 7 - q;
+        J = 8 * tr + m;
+      } else {
+        I = 8 * tr + q;
+        J = 8 * tr + 8 - m;
+      }
+    }
+  };
+  constexpr int nm = role == 0 ? 8 : 9;
+  f32x16 acc[nm];
+#pragma unroll
+  for (int m = 0; m < nm; ++m) acc[m] = f32x16{0.f};
+  issue(0);
+  if (NS > 1) issue(1);
+#pragma unroll 1
+  for (int kb = 0; kb < NS; ++kb) {
+    vm_wait(kb + 1 < NS ? 6 : 0);
+    w3_barrier();
+    if (kb + 2 < NS) issue(kb + 2);
+    const char* st = ws_lds + (kb % WS_STG) * WS_STAGE;
+    auto frag = [&](int t, bf16x8(&f)[3]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        f[p] = *reinterpret_cast<const bf16x8*>(st + ((t * 3 + p) * 64 + lane) * 16);
+    };
+    if constexpr (role == 0) {
+      bf16x8 A0[3], A1[3];
+      const int i0 = 8 + 2 * (wave >> 1);
+      frag(i0, A0);
+      frag(i0 + 1, A1);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bf16x8 B[3];
+        frag(4 * (wave & 1) + c, B);
+        if (i0 < te) acc[c] = mfma_x6(A0, B, acc[c]);
+        if (i0 + 1 < te) acc[4 + c] = mfma_x6(A1, B, acc[4 + c]);
+      }
+    } else {
+      // rows 7 - q and q of triangle tr; slot j <- tile (7 - q, j), slot
+      // 8 - j <- tile (q, j): every accumulator index static, q wave-uniform
+      const int tr = wave >> 2, q = wave & 3;
+      bf16x8 Ahi[3], Alo[3];
+      frag(8 * tr + 7 - q, Ahi);
+      frag(8 * tr + q, Alo);
+      const bool lhi = 8 * tr + 7 - q < te, llo = 8 * tr + q < te;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (j <= 7 - q) {  // wave-uniform
+          bf16x8 B[3];
+          frag(8 * tr + j, B);
+          if (lhi) acc[j] = mfma_x6(Ahi, B, acc[j]);
+          if (j <= q && llo) acc[8 - j] = mfma_x6(Alo, B, acc[8 - j]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < nm; ++m) {
+    int I, J;
+    tile_of(m, I, J);
+    float* tile = slot + (int64_t)tidx(I, J) * 1024;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int r = acc_row(q, hi);
+      tile[r * 32 + lo] = (I < te ? acc[m][q] : 0.0f) + ((I == J && r == lo) ? 1.0f : 0.0f);
+    }
+  }
+}
+
 // v = Y^T (c.*z) of one entity (z: the Cholesky output row of its slot)
 __global__ void __launch_bounds__(256) dual_wide_v_kernel(DualArgs a, const float* zb) {
   __shared__ float red[1024];
@@ -1146,9 +1271,29 @@ hipError_t launch_dual_wide(const DualArgs& a, void* zs, float* slots, float* zb
   const int64_t sf = (int64_t)dual_wide_slot_floats();
   bf16x8* z = reinterpret_cast<bf16x8*>(zs);
   hipLaunchKernelGGL(dual_wide_z_kernel, dim3((unsigned)a.n_rows), dim3(512), 0, s, a, z, slots, sf);
-  hipLaunchKernelGGL(dual_wide_s_kernel, dim3((unsigned)(a.n_rows * 10)), dim3(256), 0, s,
-                     (const bf16x8*)z, a.Dp, a.order,
-                     (int)(is_v_kind(a.kind) && a.quirk), slots, sf);
+#ifndef FRECSYS_WIDE_S_LDS_DEFAULT
+#define FRECSYS_WIDE_S_LDS_DEFAULT 1
+#endif
+  const char* sl = getenv("FRECSYS_WIDE_S_LDS");  // 0: dual_wide_s_kernel (A/B, bitwise tests)
+  if (a.Dp == 1024 && (sl ? atoi(sl) != 0 : FRECSYS_WIDE_S_LDS_DEFAULT != 0)) {
+    static bool attr = false;
+    if (!attr) {
+      for (const void* f : {(const void*)dual_wide_s_lds_kernel<0>, (const void*)dual_wide_s_lds_kernel<1>}) {
+        hipError_t err = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)WS_LDS);
+        if (err != hipSuccess) return err;
+      }
+      attr = true;
+    }
+    const int qv = (int)(is_v_kind(a.kind) && a.quirk);
+    hipLaunchKernelGGL(dual_wide_s_lds_kernel<1>, dim3((unsigned)a.n_rows), dim3(512), WS_LDS, s,
+                       (const bf16x8*)z, a.Dp, a.order, qv, slots, sf, (int64_t)a.n_rows);
+    hipLaunchKernelGGL(dual_wide_s_lds_kernel<0>, dim3((unsigned)a.n_rows), dim3(512), WS_LDS, s,
+                       (const bf16x8*)z, a.Dp, a.order, qv, slots, sf, (int64_t)a.n_rows);
+  } else {
+    hipLaunchKernelGGL(dual_wide_s_kernel, dim3((unsigned)(a.n_rows * 10)), dim3(256), 0, s,
+                       (const bf16x8*)z, a.Dp, a.order,
+                       (int)(is_v_kind(a.kind) && a.quirk), slots, sf);
+  }
   hipError_t e = launch_wide_chol_slots(a.order, a.n_rows, slots, zbuf, fail,
                                         (int)(is_v_kind(a.kind) && a.quirk), s);
   if (e != hipSuccess) return e;
