@@ -50,6 +50,10 @@
 // CU, 128 registers, 30.5 ms at MSD; 2: one workgroup, 256 registers,
 // 32.1 ms); at Dp = 1024 row p of L alone takes 128 KB of LDS: 2.
 constexpr int kWideCholWPE = 4;
+// waves of wide_chol_kernel<16>: 8 (f32 panel products, two workgroups per
+// CU); 4 with split-bf16 products (170 registers, two workgroups per CU)
+// measured MSD 114.5-115.0 vs 114.1-114.5 ms, config 5 unchanged (round 6)
+constexpr int kWideChol16NW = 8;
 
 namespace frecsys_hip {
 
@@ -734,11 +738,11 @@ __device__ __forceinline__ void wide_back_subst(float* slot, const float* yv, fl
 // against ~T^3/3 reads and T^3/3 writes of a right-looking update sweep
 // (round 2's kernel: MSD 174 GB of workspace traffic per epoch, 37 ms; this
 // one 30.5 ms).  Compiled for two workgroups per CU (128 registers).
-template <int T>
-__global__ void __launch_bounds__(512)
-    __attribute__((amdgpu_waves_per_eu(T == 16 ? kWideCholWPE : 2, 8)))
+template <int T, int NW = 8>
+__global__ void __launch_bounds__(64 * NW)
+    __attribute__((amdgpu_waves_per_eu(NW == 4 ? 2 : (T == 16 ? kWideCholWPE : 2), 8)))
     wide_chol_kernel(SolveArgs a, int64_t pos0, float* ws, int slot_out) {
-  constexpr int Dp = 32 * T, NT = T * (T + 1) / 2, NW = 8;
+  constexpr int Dp = 32 * T, NT = T * (T + 1) / 2, NTHR = 64 * NW;
   typedef float f32x4v __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) float smem[];
   // LDS tiles of row p of L and of L_pp^-1 are row-major with a 33-float
@@ -769,7 +773,7 @@ __global__ void __launch_bounds__(512)
   }
   float* slot = ws + (int64_t)blockIdx.x * ((int64_t)NT * 1024 + Dp);
   auto gtile = [&](int I, int J) { return slot + (int64_t)tidx(I, J) * 1024; };
-  for (int i = tid; i < Dp; i += 512) yv[i] = slot[(int64_t)NT * 1024 + i];
+  for (int i = tid; i < Dp; i += NTHR) yv[i] = slot[(int64_t)NT * 1024 + i];
   if (tid == 0) flag[0] = 0;
   __syncthreads();
 
@@ -782,7 +786,7 @@ __global__ void __launch_bounds__(512)
   // T = 32: split-bf16 products (common.h mfma_x6, fp32-accurate) with the
   // operands split in registers; T = 16 keeps f32 MFMA (at 128 registers the
   // splits spill, and its time was unchanged)
-  constexpr bool X6 = T == 32;
+  constexpr bool X6 = T == 32 || NW == 4;
   auto panel_sum = [&](int I, int p) __attribute__((always_inline)) {
     const float* Aip = gtile(I, p) + lo * 32 + 4 * hi;
     f32x16 c;
@@ -848,22 +852,22 @@ __global__ void __launch_bounds__(512)
     // unconditional -- past the row it re-reads tile (p, 0) and drops it --
     // so a panel costs two HBM round trips, not one per float4) ----
     {
-      constexpr int NA = ((T - 1) * 256 + 511) / 512, NB = 4;
+      constexpr int NA = ((T - 1) * 256 + NTHR - 1) / NTHR, NB = 4;
       const int n = p * 256;
 #pragma unroll
       for (int k0 = 0; k0 < NA; k0 += NB) {
-        if (tid + 512 * k0 < n) {  // wave-uniform (n is a multiple of 256)
+        if (tid + NTHR * k0 < n) {  // wave-uniform (n is a multiple of 256)
           float4 v[NB];
 #pragma unroll
           for (int k = 0; k < NB; ++k) {
-            const int i = tid + 512 * (k0 + k);
+            const int i = tid + NTHR * (k0 + k);
             const int ii = i < n ? i : tid;
             const int q = ii >> 8, r = (ii >> 3) & 31, c = (ii & 7) * 4;
             v[k] = *reinterpret_cast<const float4*>(gtile(p, q) + r * 32 + c);
           }
 #pragma unroll
           for (int k = 0; k < NB; ++k) {
-            const int i = tid + 512 * (k0 + k);
+            const int i = tid + NTHR * (k0 + k);
             if (i < n) {
               const int q = i >> 8, r = (i >> 3) & 31, c = (i & 7) * 4;
               float* t = rowL + q * LP + r * 33 + c;
@@ -965,11 +969,11 @@ __global__ void __launch_bounds__(512)
     }
     __syncthreads();
   }
-  wide_back_subst<T>(slot, yv, xv, part, wave, lo, hi, te);
+  wide_back_subst<T, NW>(slot, yv, xv, part, wave, lo, hi, te);
   // slot_out: the solution of slot b into out[Dp b ..) (the history-space
   // wide bucket's S systems), else into the entity's row
   const int64_t orow = slot_out ? (int64_t)blockIdx.x : e;
-  for (int i = tid; i < Dp; i += 512) a.out[orow * Dp + i] = i < 32 * te ? xv[i] : 0.0f;
+  for (int i = tid; i < Dp; i += NTHR) a.out[orow * Dp + i] = i < 32 * te ? xv[i] : 0.0f;
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
@@ -1571,7 +1575,7 @@ hipError_t launch_wide_chol_slots(const QueueRec* order, int64_t n, float* slots
   if (n <= 0) return hipSuccess;
   static bool attr = false;
   if (!attr) {
-    hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel<16>,
+    hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel<16, kWideChol16NW>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)wide_chol_lds_bytes(512));
     if (err != hipSuccess) return err;
@@ -1581,8 +1585,9 @@ hipError_t launch_wide_chol_slots(const QueueRec* order, int64_t n, float* slots
   a.order = order;
   a.out = out;
   a.fail = fail;
-  hipLaunchKernelGGL(wide_chol_kernel<16>, dim3((unsigned)n), dim3(512), wide_chol_lds_bytes(512),
-                     s, a, (int64_t)0, slots, quirk_v ? 2 : 1);
+  hipLaunchKernelGGL((wide_chol_kernel<16, kWideChol16NW>), dim3((unsigned)n),
+                     dim3(64 * kWideChol16NW), wide_chol_lds_bytes(512), s, a, (int64_t)0, slots,
+                     quirk_v ? 2 : 1);
   return hipGetLastError();
 }
 
@@ -1593,7 +1598,7 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
   const bool off64 = gather_off64(a.n_other, Dp);
   static bool attr = false;
   if (!attr) {
-    hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel<16>,
+    hipError_t err = hipFuncSetAttribute((const void*)wide_chol_kernel<16, kWideChol16NW>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(512));
     if (err == hipSuccess)
@@ -1642,8 +1647,8 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
     if (grad)
       hipLaunchKernelGGL(wide_grad_kernel, dim3((unsigned)nb), dim3(256), 0, s, a, Dp, s0, ws);
     else if (Dp == 512)
-      hipLaunchKernelGGL(wide_chol_kernel<16>, dim3((unsigned)nb), dim3(512),
-                         wide_chol_lds_bytes(Dp), s, a, s0, ws, 0);
+      hipLaunchKernelGGL((wide_chol_kernel<16, kWideChol16NW>), dim3((unsigned)nb),
+                         dim3(64 * kWideChol16NW), wide_chol_lds_bytes(Dp), s, a, s0, ws, 0);
     else
       hipLaunchKernelGGL(wide_chol_kernel<32>, dim3((unsigned)nb), dim3(512),
                          wide_chol_lds_bytes(Dp), s, a, s0, ws, 0);
