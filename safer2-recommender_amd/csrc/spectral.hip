@@ -1016,9 +1016,11 @@ bool rotate_lds_on() {
   return v ? atoi(v) != 0 : FRECSYS_ROT_LDS_DEFAULT != 0;
 }
 
-// rows the LDS kernel takes a launch from: fewer leave most CUs idle (one
-// 256-row block per CU), and the register-fed kernels spread them wider
-constexpr int64_t kRotLdsMinRows = 16384;
+// the LDS kernel takes a launch of at least one workgroup per CU (256-row
+// blocks x Dp / 256 column blocks: 65,536 rows at Dp = 256, 16,384 at 1024);
+// smaller ones leave most CUs idle there, and the register-fed kernels
+// spread them wider
+constexpr int64_t kRotLdsMinBlocks = 256;
 
 template <int DP, bool XB, bool QUAD>
 hipError_t launch_rotate_lds_t(const float* X, const QueueRec* rows, int64_t r0, int64_t n,
@@ -1060,7 +1062,7 @@ hipError_t launch_rotate_t(const float* X, const QueueRec* rows, int64_t r0, int
                            const bf16x8* Bs, float* Y, hipStream_t s, int xb,
                            float* qpart = nullptr) {
   if constexpr (DP % 256 == 0) {
-    if (rotate_lds_on() && n >= kRotLdsMinRows) {
+    if (rotate_lds_on() && (n / RL_ROWS) * (DP / 256) >= kRotLdsMinBlocks) {
       if (qpart) return launch_rotate_lds_t<DP, false, true>(X, nullptr, r0, n, Bs, nullptr, qpart, s);
       if (xb) return launch_rotate_lds_t<DP, true, false>(X, rows, r0, n, Bs, Y, nullptr, s);
       return launch_rotate_lds_t<DP, false, false>(X, rows, r0, n, Bs, Y, nullptr, s);

@@ -1,5 +1,5 @@
 """The rotation GEMM from LDS-DMA stages (spectral.hip rotate_lds_kernel, Dp =
-256 / 512 / 1024, launches of >= 16,384 rows) against the register-fed
+256 / 512 / 1024, launches of >= 256 blocks of 256 rows x 256 columns) against the register-fed
 rotation kernels it replaces there (FRECSYS_ROT_LDS=0): the forward rotation
 X Q of the other side, the back rotation x' Q^T of the history-space rows
 (position-blocked input, scattered output rows) and, at the wide dims, the
@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 fh = pytest.importorskip("frecsys_hip")
 from frecsys_hip.data import SynthShape, synthetic  # noqa: E402
 
-SHAPE = SynthShape(40_000, 18_000, 1_200_000, min_uc=5)
+SHAPE = SynthShape(70_000, 18_000, 2_000_000, min_uc=5)
 
 
 @pytest.fixture(scope="module")
@@ -46,7 +46,7 @@ def _epoch(data, dim):
 def test_rotate_lds_bitwise(monkeypatch, data, dim):
     monkeypatch.setenv("FRECSYS_ROT_LDS", "0")
     U0, V0, l0, nh = _epoch(data, dim)
-    assert nh >= 16384  # the back rotation of the user side takes the LDS kernel
+    assert nh >= 65536  # the back rotation of the user side takes the LDS kernel
     monkeypatch.setenv("FRECSYS_ROT_LDS", "1")
     U1, V1, l1, _ = _epoch(data, dim)
     np.testing.assert_array_equal(U1, U0)
