@@ -62,7 +62,7 @@ __device__ __forceinline__ void load_factor_rows(const lds_float* tile, int r, b
   for (int c = 0; c < 32; ++c) a[c] = fl ? a[c] : (c == r ? 1.0f : 0.0f);
 }
 
-__device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
+__device__ __forceinline__ bool diag_factor_inv_lds_body(lds_float* tile, int lane) {
   const int r = lane & 31;
   const bool fl = lane < 32;
   float a[32];
@@ -101,6 +101,9 @@ __device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
   for (int k = 0; k < 32; ++k)
     if (!fl) tile[sw(k, j)] = (k >= j) ? a[k] : 0.0f;
   return pmin > 0 && pmax <= 0x7f800000;
+}
+__device__ __noinline__ bool diag_factor_inv_lds(lds_float* tile, int lane) {
+  return diag_factor_inv_lds_body(tile, lane);
 }
 
 // Blocked form of the same factor + inverse: columns 0..15 by the

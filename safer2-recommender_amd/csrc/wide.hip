@@ -977,6 +977,553 @@ __global__ void __launch_bounds__(64 * NW)
   if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
 }
 
+// ---- the same factorisation, two panels per pass (Dp = 1024) ----
+// wide_chol_kernel streams L_Iq from the workspace once per product: at
+// Dp = 1024 the working set (2.2 MB per entity, one entity per CU) lives in
+// HBM, and its panel sums fetch 4 KB per 32x32x32 product -- ~157 GB per
+// launch at config 5, 4.1 TB/s, MFMA busy 0.21.  Here panels p and p+1 are
+// summed together, so every streamed L_Iq feeds two products:
+//   U  waves 0..6 (workers) hold C_Ip^T and C_I,p+1^T for up to 3 tiles
+//      I >= p+2 each (more tiles: another pass over q); rows p and p+1 of L
+//      come through LDS in chunks of C2_QC tiles (register-staged one chunk
+//      ahead, one barrier per chunk); L_Iq from the workspace in a 3-deep
+//      register ring.  Wave 7 (the diagonal wave) sums the diagonal block:
+//      A_pp, A_p+1,p, A_p+1,p+1 and the forward-substitution dots r_p, r_p+1.
+//   D  wave 7: L_pp^-1 (diag_factor_inv); | workers: L_Ip = C_Ip^T L_pp^-T;
+//      L_p+1,p (into LDS);                | workers: C_I,p+1 -= L_Ip L_p+1,p^T;
+//      L_p+1,p+1^-1, y_p, y_p+1;          | workers: L_I,p+1.
+// Every product, operand split and summation runs in wide_chol_kernel<T>'s
+// order on the same values (split-bf16 mfma_x6 sums over q ascending, the
+// f32 finishes, the fmaf dot chains): bit-identical to it.
+constexpr int C2_QC = 6;                   // q tiles per staged chunk
+constexpr int C2_NWK = 7, C2_NI = 2;       // worker waves, tiles per worker per pass
+constexpr int C2_RING = 6;                 // workspace tiles in flight per worker
+constexpr int C2_STAGE = 2 * C2_QC * 1024; // rows p, p+1 x QC tiles, fp32 (common.h sw layout)
+constexpr int C2_IMG = 2 * C2_QC * 3 * 32 * 16;  // their -split images: [tile][piece][row][4 x 8 bf16]
+template <int T>
+struct Chol2Lds {  // offsets in floats
+  static constexpr int Dp = 32 * T;
+  static constexpr int STG = 0;                // C2_STAGE; with IMG the finishes' transpose scratch
+  static constexpr int IMG = C2_STAGE;         // C2_IMG (floats)
+  static constexpr int LX = IMG + C2_IMG;      // L_p+1,p (sw layout)
+  static constexpr int DP0 = LX + 1024;        // L_pp^-1 (33-float rows)
+  static constexpr int DP1 = DP0 + 33 * 32;    // L_p+1,p+1^-1
+  static constexpr int DINV = DP1 + 33 * 32;   // factor tile (sw)
+  static constexpr int YV = DINV + 1024;
+  static constexpr int XV = YV + Dp;
+  static constexpr int RV = XV + Dp;           // r_p, r_p+1
+  static constexpr int PART = RV + 64;         // back-substitution partials
+  static constexpr int FLAG = PART + 8 * 32;
+  static constexpr int FLOATS = FLAG + 4;
+};
+static_assert(8 * 33 * 32 <= C2_STAGE + C2_IMG, "per-wave transpose scratch inside the stages");
+
+// -f for the three pieces of a split (sign bits: exact)
+__device__ __forceinline__ void neg3(bf16x8 (&f)[3]) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    u32x4 u = __builtin_bit_cast(u32x4, f[i]);
+    u ^= 0x80008000u;
+    f[i] = __builtin_bit_cast(bf16x8, u);
+  }
+}
+
+// Per-phase cycle counts of wide_chol2_kernel (diagnostics: build with
+// -DFRECSYS_CHOL2_PROF; workgroups 0..3 print per wave: U products, U waits
+// (DMA + chunk barriers), D work, D barrier waits, pass-start syncs)
+#ifdef FRECSYS_CHOL2_PROF
+#define C2P_DECL unsigned long long c2p_t = clock64(), c2p[5] = {0, 0, 0, 0, 0};
+#define C2P(i)                               \
+  {                                          \
+    const unsigned long long t_ = clock64(); \
+    c2p[i] += t_ - c2p_t;                    \
+    c2p_t = t_;                              \
+  }
+#define C2P_FLUSH                                                                          \
+  if (blockIdx.x < 4 && lane == 0)                                                         \
+    printf("chol2 b%d w%d U %llu Uwait %llu D %llu Dwait %llu sync %llu\n", (int)blockIdx.x, \
+           wave, c2p[0], c2p[1], c2p[2], c2p[3], c2p[4]);
+#else
+#define C2P_DECL
+#define C2P(i)
+#define C2P_FLUSH
+#endif
+
+template <int T>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+    wide_chol2_kernel(SolveArgs a, int64_t pos0, float* ws, int slot_out) {
+  using LY = Chol2Lds<T>;
+  constexpr int Dp = 32 * T, NT = T * (T + 1) / 2;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* stg = smem + LY::STG;
+  float* img = smem + LY::IMG;
+  float* lx = smem + LY::LX;
+  float* dp0 = smem + LY::DP0;
+  float* dp1 = smem + LY::DP1;
+  float* dinv = smem + LY::DINV;
+  float* yv = smem + LY::YV;
+  float* xv = smem + LY::XV;
+  float* rv = smem + LY::RV;
+  float* part = smem + LY::PART;
+  int* flag = reinterpret_cast<int*>(smem + LY::FLAG);
+  const int tid = threadIdx.x, lane = tid & 63;
+  // lo / hi are re-made opaque (fresh) at the top of each phase: otherwise the
+  // compiler hoists dozens of lane-dependent LDS / workspace offsets out of
+  // the pair loop and spills them
+  int lo = lane & 31, hi = lane >> 5;
+  auto fresh = [&]() __attribute__((always_inline)) {
+    asm volatile("" : "+v"(lo));
+    asm volatile("" : "+v"(hi));
+  };
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool dw = wave == C2_NWK;
+  const QueueRec rec = a.order[pos0 + blockIdx.x];
+  const int64_t e = rec.entity;
+  if (rec.h == 0) return;
+  int te = T;
+  if (slot_out) {
+    int64_t heff = rec.h;
+    if (slot_out == 2 && heff > 128 && (heff % 128) != 0) heff += 128 - (heff % 128);
+    te = (int)min<int64_t>(T, (heff + 31) / 32);
+  }
+  float* slot = ws + (int64_t)blockIdx.x * ((int64_t)NT * 1024 + Dp);
+  auto gtile = [&](int I, int J) { return slot + (int64_t)tidx(I, J) * 1024; };
+  for (int i = tid; i < Dp; i += 512) yv[i] = slot[(int64_t)NT * 1024 + i];
+  if (tid == 0) flag[0] = 0;
+  C2P_DECL
+
+  // row lo of an LDS tile (sw layout), columns 16 g + 8 hi + t: the bf16
+  // MFMA operand's k order
+  auto prow8 = [&](const float* t, int g, float (&v)[8]) __attribute__((always_inline)) {
+    const f32x4v a0 = row_gran(t, lo, 4 * g + 2 * hi), a1 = row_gran(t, lo, 4 * g + 2 * hi + 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = a0[j];
+      v[4 + j] = a1[j];
+    }
+  };
+  // row lo of L_Iq from the workspace in the same k order
+  auto ld_op = [&](int I, int q, f32x4v(&dst)[4]) __attribute__((always_inline)) {
+    const float* L = gtile(I, q) + lo * 32 + 8 * hi;
+    dst[0] = *reinterpret_cast<const f32x4v*>(L);
+    dst[1] = *reinterpret_cast<const f32x4v*>(L + 4);
+    dst[2] = *reinterpret_cast<const f32x4v*>(L + 16);
+    dst[3] = *reinterpret_cast<const f32x4v*>(L + 20);
+  };
+  // C^T of a panel tile as wide_chol_kernel's panel_sum starts it: A_IJ^T
+  auto ld_panel = [&](int I, int J) __attribute__((always_inline)) {
+    const float* Aip = gtile(I, J) + lo * 32 + 4 * hi;
+    f32x16 c;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4v v = *reinterpret_cast<const f32x4v*>(Aip + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[4 * g + j] = v[j];
+    }
+    return c;
+  };
+  auto ld_diag = [&](int P) __attribute__((always_inline)) {
+    const float* App = gtile(P, P);
+    f32x16 d;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[q] = App[acc_row(q, hi) * 32 + lo];
+    return d;
+  };
+  // C^T L^-T with L^-1 in a 33-float-row LDS tile (f32 MFMA, as wide_chol_kernel)
+  auto finish = [&](const f32x16& c, const float* dpad) __attribute__((always_inline)) {
+    f32x16 l = f32x16{0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < 16; ++s2) l = mfma32(c[s2], dpad[lo * 33 + acc_row(s2, hi)], l);
+    return l;
+  };
+  auto store_tile = [&](float* t, const f32x16& l) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) t[acc_row(q, hi) * 32 + lo] = l[q];
+  };
+  // D: factor + invert the diagonal tile d (wave 7): L^-1 to the workspace
+  // tile and the padded LDS copy
+  auto factor = [&](const f32x16& d, float* Aw, float* dpad) __attribute__((always_inline)) {
+    int lo_o, hi_o;  // opaque lane coordinates (wide_chol_kernel)
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lo_o) : "v"(lo));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(hi_o) : "v"(hi));
+#pragma unroll
+    for (int q = 0; q < 16; ++q) dinv[sw(acc_row(q, hi_o), lo_o)] = d[q];
+    wave_lds_sync();
+    // inlined (as a call, every worker accumulator live across it would be
+    // saved to scratch around it)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    if (!diag_factor_inv_lds_body((lds_float*)dinv, ln) && lane == 0) flag[0] = 1;
+    wave_lds_sync();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = 2 * i + hi_o;
+      const float v = dinv[sw(r, lo_o)];
+      Aw[r * 32 + lo_o] = v;
+      dpad[r * 33 + lo_o] = v;
+    }
+  };
+  // y_P = L_PP^-1 r (wave 7)
+  auto fwd = [&](const float* dpad, const float* r, int P) __attribute__((always_inline)) {
+    float y = 0.0f;
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) y = __builtin_fmaf(dpad[lo * 33 + 16 * hi + k2], r[16 * hi + k2], y);
+    y += __shfl_xor(y, 32);
+    if (hi == 0) yv[32 * P + lo] = y;
+  };
+  __syncthreads();
+
+  // rows p, p+1 of L (tiles q < p) through LDS in chunks of C2_QC tiles, by
+  // LDS-DMA (no registers): 2 C2_QC tiles x 4 wave-instructions of 1 KB,
+  // C2_DMA per wave; LDS position pos of a tile holds the granule that
+  // common.h sw puts there.  Out-of-range tiles re-read tile p-1 (never read
+  // back), so every wave issues exactly C2_DMA loads per chunk
+  constexpr int C2_DMA = 2 * C2_QC * 4 / 8;
+  auto stage_dma = [&](int p, bool two, int ch) __attribute__((always_inline)) {
+    float* st = stg;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int k = 0; k < C2_DMA; ++k) {
+      const int f = C2_DMA * wave + k;  // wave-uniform
+      const int ti = f >> 2, i = f & 3;
+      const int sel = ti >= C2_QC, qo = ti - C2_QC * sel;
+      const int q = min(C2_QC * ch + qo, p - 1);
+      const int pos = 64 * i + ln, r = pos >> 3, G = (pos & 7) ^ ((r >> 1) & 7);
+      glds16(gtile(p + (two ? sel : 0), q) + r * 32 + 4 * G,
+             lds_addr(st + sel * C2_QC * 1024 + qo * 1024 + 256 * i));
+    }
+  };
+  // the chunk in the stage -> its negated 3-piece split image (each worker
+  // would otherwise split the same rows for every tile it owns): unit =
+  // (tile, row, 8 columns), 3 per thread; 16-B granule kg of a row sits at
+  // kg ^ ((row >> 2) & 3) (lanes over rows read conflict-free)
+  auto split_chunk = [&]() __attribute__((always_inline)) {
+    int t = tid;
+    asm volatile("" : "+v"(t));
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int unit = t + 512 * u, ti = unit >> 7, r = (unit >> 2) & 31, kg = unit & 3;
+      const float* src = stg + ti * 1024;
+      const f32x4v a0 = row_gran(src, r, 2 * kg), a1 = row_gran(src, r, 2 * kg + 1);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = a0[j];
+        v[4 + j] = a1[j];
+      }
+      bf16x8 f[3];
+      split3x8(v, f);
+      neg3(f);
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc)
+        *reinterpret_cast<bf16x8*>(img + (((ti * 3 + pc) * 32 + r) * 4 + (kg ^ ((r >> 2) & 3))) * 4) = f[pc];
+    }
+  };
+  // -split(row lo of image tile ti), k = 16 g + 8 hi .. +7: the MFMA A operand
+  auto img_frag = [&](int ti, int g, bf16x8(&f)[3]) __attribute__((always_inline)) {
+    const int kg = 2 * g + hi;
+#pragma unroll
+    for (int pc = 0; pc < 3; ++pc)
+      f[pc] = *reinterpret_cast<const bf16x8*>(img + (((ti * 3 + pc) * 32 + lo) * 4 + (kg ^ ((lo >> 2) & 3))) * 4);
+  };
+  // U for one role; every role runs the same barriers.  NV = -1: the
+  // diagonal wave (d0 = c1[0], cx = c2[0], d1 = c1[1]); NV = 0..C2_NI: a
+  // worker with NV tiles, all valid (the tile count is a compile-time
+  // constant: no per-tile branches, so no register copies at the joins)
+  auto uphase = [&](auto nv_c, int p, bool two, int tb, f32x16(&c1)[C2_NI], f32x16(&c2)[C2_NI],
+                    float& r0, float& r1) __attribute__((always_inline)) {
+    constexpr int NV = decltype(nv_c)::value;
+    // ring: C2_RING workspace tiles in flight, D = C2_RING / NV steps of q
+    // per block (the q loop unrolled by D, so every ring slot is static)
+    constexpr int D = NV > 0 ? C2_RING / NV : 1;
+    static_assert(NV <= 0 || (C2_RING % NV == 0 && C2_QC % D == 0), "ring blocks tile the chunks");
+    const int nch = (p + C2_QC - 1) / C2_QC;
+    f32x4v ring[NV > 0 ? NV : 1][D][4];
+    // the first chunk before the ring's first loads: a worker's wait for it
+    // then leaves those 4 NV D loads in flight
+    if (nch > 0) stage_dma(p, two, 0);
+    if constexpr (NV > 0) {
+#pragma unroll
+      for (int s = 0; s < NV; ++s) {
+        c1[s] = ld_panel(p + 2 + tb + C2_NWK * s, p);
+        c2[s] = ld_panel(p + 2 + tb + C2_NWK * s, p + 1);
+        if (p > 0) {
+#pragma unroll
+          for (int d = 0; d < D; ++d) ld_op(p + 2 + tb + C2_NWK * s, min(d, p - 1), ring[s][d]);
+        }
+      }
+    }
+    if constexpr (NV == -1) {
+      c1[0] = ld_diag(p);
+      if (two) {
+        c2[0] = ld_panel(p + 1, p);
+        c1[1] = ld_diag(p + 1);
+      }
+    }
+    C2P(0)
+    vm_wait(NV > 0 && p > 0 ? 4 * NV * D : 0);
+    lds_barrier();
+    C2P(1)
+#pragma unroll 1
+    for (int ch = 0; ch < nch; ++ch) {
+      const int q0 = C2_QC * ch, q1 = min(p, q0 + C2_QC);
+      // the stage holds chunk ch: its image, and (diagonal wave) the
+      // forward-substitution dots r_P -= L_Pq y_q, row lo, k = 16 hi + k2
+      // (wide_chol_kernel's chain), which need the fp32 rows
+      fresh();
+      split_chunk();
+      if constexpr (NV == -1) {
+#pragma unroll 1
+        for (int q = q0; q < q1; ++q) {
+          const float* t0 = stg + (q - q0) * 1024;  // L_pq
+          const float* t1 = t0 + C2_QC * 1024;      // L_p+1,q
+#pragma unroll
+          for (int G = 0; G < 4; ++G) {
+            const f32x4v a0 = row_gran(t0, lo, 4 * hi + G);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r0 = __builtin_fmaf(a0[j], yv[32 * q + 16 * hi + 4 * G + j], r0);
+          }
+          if (two) {
+#pragma unroll
+            for (int G = 0; G < 4; ++G) {
+              const f32x4v a1 = row_gran(t1, lo, 4 * hi + G);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) r1 = __builtin_fmaf(a1[j], yv[32 * q + 16 * hi + 4 * G + j], r1);
+            }
+          }
+        }
+      }
+      C2P(0)
+      lds_barrier();  // the image is complete, the stage free
+      C2P(1)
+      if (ch + 1 < nch) stage_dma(p, two, ch + 1);
+      if constexpr (NV == -1) {
+#pragma unroll 1
+        for (int q = q0; q < q1; ++q) {
+          fresh();
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            bf16x8 nf0[3], pf0[3];
+            img_frag(q - q0, g, nf0);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) pf0[i] = nf0[i];
+            neg3(pf0);
+            c1[0] = mfma_x6(nf0, pf0, c1[0]);
+            if (two) {
+              bf16x8 nf1[3], pf1[3];
+              img_frag(C2_QC + q - q0, g, nf1);
+#pragma unroll
+              for (int i = 0; i < 3; ++i) pf1[i] = nf1[i];
+              neg3(pf1);
+              c2[0] = mfma_x6(nf0, pf1, c2[0]);
+              c1[1] = mfma_x6(nf1, pf1, c1[1]);
+            }
+          }
+        }
+      } else if constexpr (NV > 0) {
+#pragma unroll 1
+        for (int qb = q0; qb < q1; qb += D) {
+#pragma unroll
+          for (int d = 0; d < D; ++d) {
+            const int q = qb + d;
+            fresh();
+            if (q < q1) {  // wave-uniform; only the pair's last block is partial
+#pragma unroll
+              for (int s = 0; s < NV; ++s) {
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                  float lv[8];
+#pragma unroll
+                  for (int t = 0; t < 8; ++t) lv[t] = ring[s][d][2 * g + (t >> 2)][t & 3];
+                  bf16x8 lf[3], pf[3];
+                  split3x8(lv, lf);
+                  img_frag(q - q0, g, pf);
+                  c1[s] = mfma_x6(pf, lf, c1[s]);
+                  img_frag(C2_QC + q - q0, g, pf);
+                  c2[s] = mfma_x6(pf, lf, c2[s]);
+                  __builtin_amdgcn_sched_barrier(0);  // one (tile, g) of operands live at a time
+                }
+              }
+            }
+            // tile q + D into the slot just read; unconditional (past the end
+            // it re-reads tile p-1), so that no register phi forms at the joins
+#pragma unroll
+            for (int s = 0; s < NV; ++s) ld_op(p + 2 + tb + C2_NWK * s, min(q + D, p - 1), ring[s][d]);
+          }
+        }
+      }
+      // chunk ch+1 landed: only this chunk's ring loads (4 per tile and step,
+      // every step of a block issues them) may still be in flight
+      C2P(0)
+      if (ch + 1 < nch) vm_wait(NV > 0 ? 4 * NV * D * ((q1 - q0 + D - 1) / D) : 0);
+      lds_barrier();
+      C2P(1)
+    }
+  };
+  // D for a worker with NV tiles (barriers B1-B3 only in the first pass,
+  // where the diagonal wave produces what they wait for)
+  auto wphase = [&](auto nv_c, int p, bool two, int tb, bool first, f32x16(&c1)[C2_NI],
+                    f32x16(&c2)[C2_NI]) __attribute__((always_inline)) {
+    constexpr int NV = decltype(nv_c)::value;
+    float* scr = stg + wave * 33 * 32;  // the stages are free now
+    C2P(2)
+    if (first) lds_barrier();  // B1: L_pp^-1
+    C2P(3)
+    fresh();
+#pragma unroll
+    for (int s = 0; s < NV; ++s) {
+      c1[s] = finish(c1[s], dp0);  // L_Ip
+      store_tile(gtile(p + 2 + tb + C2_NWK * s, p), c1[s]);
+    }
+    if (two) {
+      C2P(2)
+      if (first) lds_barrier();  // B2: L_p+1,p
+      C2P(3)
+      // C_I,p+1 -= L_Ip L_p+1,p^T: L_Ip to operand order through the scratch
+#pragma unroll
+      for (int s = 0; s < NV; ++s) {
+        fresh();
+#pragma unroll
+        for (int q = 0; q < 16; ++q) scr[acc_row(q, hi) * 33 + lo] = c1[s][q];
+        wave_lds_sync();
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          float lv[8], pv[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) lv[t] = scr[lo * 33 + 16 * g + 8 * hi + t];
+          bf16x8 lf[3], pf[3];
+          split3x8(lv, lf);
+          prow8(lx, g, pv);
+          split3x8(pv, pf);
+          neg3(pf);
+          c2[s] = mfma_x6(pf, lf, c2[s]);
+        }
+        wave_lds_sync();
+      }
+      C2P(2)
+      if (first) lds_barrier();  // B3: L_p+1,p+1^-1
+      C2P(3)
+      fresh();
+#pragma unroll
+      for (int s = 0; s < NV; ++s) store_tile(gtile(p + 2 + tb + C2_NWK * s, p + 1), finish(c2[s], dp1));
+    }
+  };
+  // D for the diagonal wave: both factorisations through one inlined copy
+  // of the factor (two copies overflow the SGPRs)
+  auto dphase = [&](int p, bool two, f32x16(&c1)[C2_NI], f32x16(&c2)[C2_NI], float r0,
+                    float r1) __attribute__((always_inline)) {
+#pragma unroll 1
+    for (int it = 0; it < (two ? 2 : 1); ++it) {
+      fresh();
+      if (it == 1) {
+        wave_lds_sync();
+        fwd(dp0, rv, p);
+        wave_lds_sync();
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {  // the q = p term of A_p+1,p+1
+          float v[8];
+          prow8(lx, g, v);
+          bf16x8 pf[3], nf[3];
+          split3x8(v, pf);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) nf[i] = pf[i];
+          neg3(nf);
+          c1[1] = mfma_x6(nf, pf, c1[1]);
+        }
+#pragma unroll
+        for (int G = 0; G < 4; ++G) {
+          const f32x4v a1 = row_gran(lx, lo, 4 * hi + G);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) r1 = __builtin_fmaf(a1[j], yv[32 * p + 16 * hi + 4 * G + j], r1);
+        }
+      }
+      f32x16 dd;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) dd[q] = it == 0 ? c1[0][q] : c1[1][q];
+      factor(dd, gtile(p + it, p + it), it == 0 ? dp0 : dp1);
+      float rr = it == 0 ? r0 : r1;
+      rr += __shfl_xor(rr, 32);
+      if (hi == 0) rv[32 * it + lo] = yv[32 * (p + it) + lo] - rr;
+      if (it == 0) {
+        C2P(2)
+        lds_barrier();  // B1
+        C2P(3)
+        if (two) {
+          fresh();
+          const f32x16 l = finish(c2[0], dp0);  // L_p+1,p
+          store_tile(gtile(p + 1, p), l);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) lx[sw(acc_row(q, hi), lo)] = l[q];
+          C2P(2)
+          lds_barrier();  // B2
+          C2P(3)
+        }
+      } else {
+        C2P(2)
+        lds_barrier();  // B3
+        C2P(3)
+      }
+    }
+    wave_lds_sync();
+    if (two) fwd(dp1, rv + 32, p + 1);
+    else fwd(dp0, rv, p);
+  };
+  typedef std::integral_constant<int, -1> DiagRole;
+  typedef std::integral_constant<int, 0> Idle;
+  typedef std::integral_constant<int, 1> One;
+  typedef std::integral_constant<int, 2> Two;
+  static_assert(C2_NI == 2, "role dispatch below");
+
+#pragma unroll 1
+  for (int p = 0; p < te; p += 2) {
+    const bool two = p + 1 < te;
+    const int nI = te - p - 2;  // tiles below the pair (workers have tiles only with two)
+    const int npass = nI > C2_NWK * C2_NI ? (nI + C2_NWK * C2_NI - 1) / (C2_NWK * C2_NI) : 1;
+#pragma unroll 1
+    for (int pass = 0; pass < npass; ++pass) {
+      C2P(2)
+      __syncthreads();  // the last pass's workspace stores and scratch reads are done
+      C2P(4)
+      fresh();
+      const int tb = C2_NWK * C2_NI * pass + wave;
+      const bool first = pass == 0;
+      const int nv = dw ? 0 : max(0, min(C2_NI, (nI - tb + C2_NWK - 1) / C2_NWK));
+      // each role's registers are its own (shared arrays would meet at the
+      // joins with undefined parts, which the compiler keeps as zeros)
+      if (dw && first) {
+        f32x16 c1[C2_NI], c2[C2_NI];
+        float r0 = 0.0f, r1 = 0.0f;
+        uphase(DiagRole{}, p, two, tb, c1, c2, r0, r1);
+        dphase(p, two, c1, c2, r0, r1);
+      } else if (nv == 2) {
+        f32x16 c1[C2_NI], c2[C2_NI];
+        float r0 = 0.0f, r1 = 0.0f;
+        uphase(Two{}, p, two, tb, c1, c2, r0, r1);
+        wphase(Two{}, p, two, tb, first, c1, c2);
+      } else if (nv == 1) {
+        f32x16 c1[C2_NI], c2[C2_NI];
+        float r0 = 0.0f, r1 = 0.0f;
+        uphase(One{}, p, two, tb, c1, c2, r0, r1);
+        wphase(One{}, p, two, tb, first, c1, c2);
+      } else {
+        f32x16 c1[C2_NI], c2[C2_NI];
+        float r0 = 0.0f, r1 = 0.0f;
+        uphase(Idle{}, p, two, tb, c1, c2, r0, r1);
+        wphase(Idle{}, p, two, tb, first, c1, c2);
+      }
+    }
+  }
+  C2P(2)
+  C2P_FLUSH
+  __syncthreads();
+  wide_back_subst<T, 8>(slot, yv, xv, part, wave, lo, hi, te);
+  const int64_t orow = slot_out ? (int64_t)blockIdx.x : e;
+  for (int i = tid; i < Dp; i += 512) a.out[orow * Dp + i] = i < 32 * te ? xv[i] : 0.0f;
+  if (tid == 0 && flag[0]) atomicMin(a.fail, (unsigned long long)(e + 1));
+}
+
 // CVaR-MF: x = e - eta (A_full e - b), A_full's strict upper part the stale
 // G part (cvar_upper); one workgroup per entity.
 __global__ void __launch_bounds__(256)
@@ -1520,6 +2067,16 @@ __global__ void __launch_bounds__(256) loss_gather_wide_kernel(LossArgs a) {
 }
 
 
+// the two-panel Cholesky at Dp = 1024 (FRECSYS_WIDE_CHOL2=0: the one-panel
+// kernel, A/B; bit-identical)
+#ifndef FRECSYS_WIDE_CHOL2_DEFAULT
+#define FRECSYS_WIDE_CHOL2_DEFAULT 1
+#endif
+bool wide_chol2_on() {
+  const char* v = getenv("FRECSYS_WIDE_CHOL2");
+  return v ? atoi(v) != 0 : FRECSYS_WIDE_CHOL2_DEFAULT != 0;
+}
+
 size_t wide_chol_lds_bytes(int Dp) {
   const int T = Dp >> 5;
   return sizeof(float) * ((size_t)T * 33 * 32 + 1024 + 2 * Dp + 32 + 8 * 32 + 4);
@@ -1605,9 +2162,14 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
       err = hipFuncSetAttribute((const void*)wide_chol_kernel<32>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(1024));
+    if (err == hipSuccess)
+      err = hipFuncSetAttribute((const void*)wide_chol2_kernel<32>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(sizeof(float) * Chol2Lds<32>::FLOATS));
     if (err != hipSuccess) return err;
     attr = true;
   }
+  const bool chol2 = wide_chol2_on();
   const bool grad = is_grad_kind(a.kind);
   GramArgs g{};
   // the SYRK from the pre-split table (wide_syrk.hip; xsplit: its buffer,
@@ -1649,6 +2211,9 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
     else if (Dp == 512)
       hipLaunchKernelGGL((wide_chol_kernel<16, kWideChol16NW>), dim3((unsigned)nb),
                          dim3(64 * kWideChol16NW), wide_chol_lds_bytes(Dp), s, a, s0, ws, 0);
+    else if (chol2)
+      hipLaunchKernelGGL(wide_chol2_kernel<32>, dim3((unsigned)nb), dim3(512),
+                         sizeof(float) * Chol2Lds<32>::FLOATS, s, a, s0, ws, 0);
     else
       hipLaunchKernelGGL(wide_chol_kernel<32>, dim3((unsigned)nb), dim3(512),
                          wide_chol_lds_bytes(Dp), s, a, s0, ws, 0);
