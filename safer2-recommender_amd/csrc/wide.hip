@@ -995,28 +995,39 @@ __global__ void __launch_bounds__(64 * NW)
 // Every product, operand split and summation runs in wide_chol_kernel<T>'s
 // order on the same values (split-bf16 mfma_x6 sums over q ascending, the
 // f32 finishes, the fmaf dot chains): bit-identical to it.
-constexpr int C2_QC = 6;                   // q tiles per staged chunk
-constexpr int C2_NWK = 7, C2_NI = 2;       // worker waves, tiles per worker per pass
-constexpr int C2_RING = 6;                 // workspace tiles in flight per worker
-constexpr int C2_STAGE = 2 * C2_QC * 1024; // rows p, p+1 x QC tiles, fp32 (common.h sw layout)
-constexpr int C2_IMG = 2 * C2_QC * 3 * 32 * 16;  // their -split images: [tile][piece][row][4 x 8 bf16]
-template <int T>
+// Configuration (every one bit-identical): QC q tiles per staged chunk, NI
+// tiles per worker per pass, RING workspace tiles in flight per worker, WPE
+// waves per SIMD the registers are sized for.  Measured at config 5,
+// streams serialised: <6, 2, 6, 2> (one workgroup per CU, 256 registers)
+// 26.8 ms per launch; <2, 1, 2, 4> (two workgroups per CU, 128 registers,
+// 66 KB of LDS each) 30.6 ms; the one-panel kernel 31.9 ms
+// (profiles/r06/wide_chol2/)
+template <int QC_, int NI_, int RING_, int WPE_>
+struct Chol2Cfg {
+  static constexpr int QC = QC_, NI = NI_, RING = RING_, WPE = WPE_;
+  static constexpr int STAGE = 2 * QC * 1024;       // rows p, p+1 x QC tiles, fp32 (common.h sw)
+  static constexpr int IMG = 2 * QC * 3 * 32 * 16;  // their -split images: [tile][piece][row][4 x 8 bf16]
+  static_assert(QC % 2 == 0, "split units: QC / 2 per thread");
+  static_assert(8 * 33 * 32 <= STAGE + IMG, "per-wave transpose scratch inside the stages");
+};
+typedef Chol2Cfg<6, 2, 6, 2> Chol2Wide;
+constexpr int C2_NWK = 7;                // worker waves (wave 7: the diagonal wave)
+template <int T, class CF>
 struct Chol2Lds {  // offsets in floats
   static constexpr int Dp = 32 * T;
-  static constexpr int STG = 0;                // C2_STAGE; with IMG the finishes' transpose scratch
-  static constexpr int IMG = C2_STAGE;         // C2_IMG (floats)
-  static constexpr int LX = IMG + C2_IMG;      // L_p+1,p (sw layout)
-  static constexpr int DP0 = LX + 1024;        // L_pp^-1 (33-float rows)
-  static constexpr int DP1 = DP0 + 33 * 32;    // L_p+1,p+1^-1
-  static constexpr int DINV = DP1 + 33 * 32;   // factor tile (sw)
+  static constexpr int STG = 0;             // CF::STAGE; with IMG the finishes' transpose scratch
+  static constexpr int IMG = CF::STAGE;     // CF::IMG (floats)
+  static constexpr int LX = IMG + CF::IMG;  // L_p+1,p (sw layout)
+  static constexpr int DP0 = LX + 1024;     // L_pp^-1 (33-float rows)
+  static constexpr int DP1 = DP0 + 33 * 32; // L_p+1,p+1^-1
+  static constexpr int DINV = DP1 + 33 * 32;  // factor tile (sw)
   static constexpr int YV = DINV + 1024;
   static constexpr int XV = YV + Dp;
-  static constexpr int RV = XV + Dp;           // r_p, r_p+1
-  static constexpr int PART = RV + 64;         // back-substitution partials
+  static constexpr int RV = XV + Dp;        // r_p, r_p+1
+  static constexpr int PART = RV + 64;      // back-substitution partials
   static constexpr int FLAG = PART + 8 * 32;
   static constexpr int FLOATS = FLAG + 4;
 };
-static_assert(8 * 33 * 32 <= C2_STAGE + C2_IMG, "per-wave transpose scratch inside the stages");
 
 // -f for the three pieces of a split (sign bits: exact)
 __device__ __forceinline__ void neg3(bf16x8 (&f)[3]) {
@@ -1050,10 +1061,13 @@ __device__ __forceinline__ void neg3(bf16x8 (&f)[3]) {
 #define C2P_FLUSH
 #endif
 
-template <int T>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+template <int T, class CF>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(CF::WPE, CF::WPE)))
     wide_chol2_kernel(SolveArgs a, int64_t pos0, float* ws, int slot_out) {
-  using LY = Chol2Lds<T>;
+  using LY = Chol2Lds<T, CF>;
+  constexpr int C2_QC = CF::QC, C2_NI = CF::NI, C2_RING = CF::RING;
+  constexpr int C2_NA = C2_NI > 2 ? C2_NI : 2;  // accumulator arrays (the diagonal wave uses 3)
+  constexpr int C2_STAGE = CF::STAGE;
   constexpr int Dp = 32 * T, NT = T * (T + 1) / 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* stg = smem + LY::STG;
@@ -1203,7 +1217,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     int t = tid;
     asm volatile("" : "+v"(t));
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
+    for (int u = 0; u < C2_QC / 2; ++u) {
       const int unit = t + 512 * u, ti = unit >> 7, r = (unit >> 2) & 31, kg = unit & 3;
       const float* src = stg + ti * 1024;
       const f32x4v a0 = row_gran(src, r, 2 * kg), a1 = row_gran(src, r, 2 * kg + 1);
@@ -1232,7 +1246,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // diagonal wave (d0 = c1[0], cx = c2[0], d1 = c1[1]); NV = 0..C2_NI: a
   // worker with NV tiles, all valid (the tile count is a compile-time
   // constant: no per-tile branches, so no register copies at the joins)
-  auto uphase = [&](auto nv_c, int p, bool two, int tb, f32x16(&c1)[C2_NI], f32x16(&c2)[C2_NI],
+  auto uphase = [&](auto nv_c, int p, bool two, int tb, f32x16(&c1)[C2_NA], f32x16(&c2)[C2_NA],
                     float& r0, float& r1) __attribute__((always_inline)) {
     constexpr int NV = decltype(nv_c)::value;
     // ring: C2_RING workspace tiles in flight, D = C2_RING / NV steps of q
@@ -1364,8 +1378,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   };
   // D for a worker with NV tiles (barriers B1-B3 only in the first pass,
   // where the diagonal wave produces what they wait for)
-  auto wphase = [&](auto nv_c, int p, bool two, int tb, bool first, f32x16(&c1)[C2_NI],
-                    f32x16(&c2)[C2_NI]) __attribute__((always_inline)) {
+  auto wphase = [&](auto nv_c, int p, bool two, int tb, bool first, f32x16(&c1)[C2_NA],
+                    f32x16(&c2)[C2_NA]) __attribute__((always_inline)) {
     constexpr int NV = decltype(nv_c)::value;
     float* scr = stg + wave * 33 * 32;  // the stages are free now
     C2P(2)
@@ -1412,7 +1426,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   };
   // D for the diagonal wave: both factorisations through one inlined copy
   // of the factor (two copies overflow the SGPRs)
-  auto dphase = [&](int p, bool two, f32x16(&c1)[C2_NI], f32x16(&c2)[C2_NI], float r0,
+  auto dphase = [&](int p, bool two, f32x16(&c1)[C2_NA], f32x16(&c2)[C2_NA], float r0,
                     float r1) __attribute__((always_inline)) {
 #pragma unroll 1
     for (int it = 0; it < (two ? 2 : 1); ++it) {
@@ -1474,7 +1488,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   typedef std::integral_constant<int, 0> Idle;
   typedef std::integral_constant<int, 1> One;
   typedef std::integral_constant<int, 2> Two;
-  static_assert(C2_NI == 2, "role dispatch below");
+  static_assert(C2_NI == 1 || C2_NI == 2, "role dispatch below");
 
 #pragma unroll 1
   for (int p = 0; p < te; p += 2) {
@@ -1493,22 +1507,22 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       // each role's registers are its own (shared arrays would meet at the
       // joins with undefined parts, which the compiler keeps as zeros)
       if (dw && first) {
-        f32x16 c1[C2_NI], c2[C2_NI];
+        f32x16 c1[C2_NA], c2[C2_NA];
         float r0 = 0.0f, r1 = 0.0f;
         uphase(DiagRole{}, p, two, tb, c1, c2, r0, r1);
         dphase(p, two, c1, c2, r0, r1);
-      } else if (nv == 2) {
-        f32x16 c1[C2_NI], c2[C2_NI];
+      } else if (C2_NI >= 2 && nv == 2) {
+        f32x16 c1[C2_NA], c2[C2_NA];
         float r0 = 0.0f, r1 = 0.0f;
-        uphase(Two{}, p, two, tb, c1, c2, r0, r1);
-        wphase(Two{}, p, two, tb, first, c1, c2);
+        uphase(std::integral_constant<int, (C2_NI >= 2 ? 2 : 1)>{}, p, two, tb, c1, c2, r0, r1);
+        wphase(std::integral_constant<int, (C2_NI >= 2 ? 2 : 1)>{}, p, two, tb, first, c1, c2);
       } else if (nv == 1) {
-        f32x16 c1[C2_NI], c2[C2_NI];
+        f32x16 c1[C2_NA], c2[C2_NA];
         float r0 = 0.0f, r1 = 0.0f;
         uphase(One{}, p, two, tb, c1, c2, r0, r1);
         wphase(One{}, p, two, tb, first, c1, c2);
       } else {
-        f32x16 c1[C2_NI], c2[C2_NI];
+        f32x16 c1[C2_NA], c2[C2_NA];
         float r0 = 0.0f, r1 = 0.0f;
         uphase(Idle{}, p, two, tb, c1, c2, r0, r1);
         wphase(Idle{}, p, two, tb, first, c1, c2);
@@ -2163,9 +2177,9 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_chol_lds_bytes(1024));
     if (err == hipSuccess)
-      err = hipFuncSetAttribute((const void*)wide_chol2_kernel<32>,
+      err = hipFuncSetAttribute((const void*)wide_chol2_kernel<32, Chol2Wide>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(float) * Chol2Lds<32>::FLOATS));
+                                (int)(sizeof(float) * Chol2Lds<32, Chol2Wide>::FLOATS));
     if (err != hipSuccess) return err;
     attr = true;
   }
@@ -2212,8 +2226,8 @@ hipError_t launch_wide_solve(int Dp, const SolveArgs& a, float* ws, int64_t batc
       hipLaunchKernelGGL((wide_chol_kernel<16, kWideChol16NW>), dim3((unsigned)nb),
                          dim3(64 * kWideChol16NW), wide_chol_lds_bytes(Dp), s, a, s0, ws, 0);
     else if (chol2)
-      hipLaunchKernelGGL(wide_chol2_kernel<32>, dim3((unsigned)nb), dim3(512),
-                         sizeof(float) * Chol2Lds<32>::FLOATS, s, a, s0, ws, 0);
+      hipLaunchKernelGGL((wide_chol2_kernel<32, Chol2Wide>), dim3((unsigned)nb), dim3(512),
+                         (sizeof(float) * Chol2Lds<32, Chol2Wide>::FLOATS), s, a, s0, ws, 0);
     else
       hipLaunchKernelGGL(wide_chol_kernel<32>, dim3((unsigned)nb), dim3(512),
                          wide_chol_lds_bytes(Dp), s, a, s0, ws, 0);
