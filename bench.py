@@ -458,8 +458,9 @@ def run_workload(name, args, world, rank, local_rank, dist, data_cache, steps, w
         "roofline": {"bound": "mfma",
                      "kernel": ("wide_syrk3_kernel<2> (slabs of the long histories) + "
                                 "wide_syrk3_kernel<1> (split-bf16 MFMA SYRK from the pre-split "
-                                "table) + wide_chol_kernel<16> (batched d-space solve, A in an "
-                                "HBM workspace)") if wide else
+                                "table) + " + ("wide_chol2_kernel<32> (two-panel" if Dp == 1024
+                                               else "wide_chol_kernel<16> (") +
+                                " batched d-space Cholesky, A in an HBM workspace)") if wide else
                                ("solve_tiled_kernel<8, false, true> (d-space solve: split-bf16 "
                                 "MFMA SYRK + fp32 dataflow Cholesky)"),
                      "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",

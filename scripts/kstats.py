@@ -10,7 +10,7 @@ tot = 0.0
 for r in rows:
     tot += float(r["TotalDurationNs"])
 for r in rows[:top]:
-    short = r["Name"].split("(anonymous namespace)::")[-1][:58]
+    short = r["Name"].replace("frecsys_hip::(anonymous namespace)::", "").removeprefix("void ")[:58]
     print(f"{short:60s} calls {r['Calls']:>5} avg_us {float(r['AverageNs']) / 1e3:9.1f} "
           f"ms/epoch {float(r['TotalDurationNs']) / 1e6 / ep:8.3f}")
 print(f"total kernel ms/epoch {tot / 1e6 / ep:.3f}")

@@ -43,7 +43,8 @@ def dominant(name, workload):
         # SYRK and Cholesky launches (wide_syrk2: FRECSYS_WIDE_PRESPLIT=0)
         return any(k in name for k in ("wide_presplit_kernel", "wide_syrk3_kernel<1",
                                        "wide_syrk3_kernel<2", "wide_syrk2_kernel<1>",
-                                       "wide_syrk2_kernel<2>", "wide_chol_kernel"))
+                                       "wide_syrk2_kernel<2>", "wide_chol_kernel",
+                                       "wide_chol2_kernel"))
     return "solve_tiled_kernel<8, false" in name
 
 

@@ -15,7 +15,7 @@ path, ncu = sys.argv[1], int(sys.argv[2])
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
 launches = collections.defaultdict(set)
 for r in csv.DictReader(open(path)):
-    name = r["Kernel_Name"].split("(anonymous namespace)::")[-1].split("(")[0]
+    name = r["Kernel_Name"].replace("frecsys_hip::(anonymous namespace)::", "").split("(")[0]
     acc[name][r["Counter_Name"]] += float(r["Counter_Value"])
     launches[name].add(r["Dispatch_Id"])
 out = {}

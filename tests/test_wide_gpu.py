@@ -151,9 +151,13 @@ def test_wide_user_loss(wide_data, dim, half):
     assert lg[5] == 0.0
 
 
-def test_wide_not_spd_reported(wide_data):
+@pytest.mark.parametrize("dim", [512, 1024])
+def test_wide_not_spd_reported(wide_data, dim, monkeypatch):
+    # every entity in d space: the wide Cholesky kernels themselves (at 1024
+    # the two-panel one) must flag the failed pivot
+    monkeypatch.setenv("FRECSYS_DUAL", "0")
     nu, ni, up, uc, ip, ic = wide_data
-    ctx, U, V = _ctx(512, nu, ni, up, uc, ip, ic)
+    ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
     ctx.gramian(fh.SIDE_ITEM)
     with pytest.raises(fh.FrecsysError) as ei:
         ctx.solve_side(fh.SIDE_USER, fh.KIND_IALS, -50.0, 0.1)
