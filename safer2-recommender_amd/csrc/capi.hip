@@ -1139,6 +1139,12 @@ int frecsys_ctx_create(const frecsys_config* cfg, frecsys_ctx** out) {
   const int max_h_cap = Dp >= 512 ? kDualWideMaxH : 32 * kDualMaxTiles;
   c->dual_max_h = std::min(c->dual_max_h, max_h_cap);
   for (int t = 0; t < 3; ++t) c->dual_max_h_side[t] = c->dual_max_h;
+  // Dp = 512, user side: 320.  That half-step is bound by its d-space stream
+  // (MSD: 45 ms beside 29 of history space), and the wide bucket takes the
+  // users with 256 < h_eff <= 320 off it: MSD 115.3 -> 114.1 ms (items: no
+  // gain; DESIGN.md 3.8, profiles/r06/dual_max_h/)
+  if (Dp == 512 && !getenv("FRECSYS_DUAL_MAX_H"))
+    c->dual_max_h_side[FRECSYS_SIDE_USER] = std::min(320, max_h_cap);
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H_USER"))
     c->dual_max_h_side[0] = std::min(atoi(v), max_h_cap);
   if (const char* v = getenv("FRECSYS_DUAL_MAX_H_ITEM"))
