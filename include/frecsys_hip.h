@@ -334,6 +334,11 @@ int frecsys_work(const frecsys_ctx* ctx, const char* what, double* flops, double
 /* Longest assembly history (h_eff) the history-space path takes on this
  * context (0: that path is off); longer histories run the d-space solve. */
 int32_t frecsys_history_space_max_h(const frecsys_ctx* ctx);
+/* The same for one solved side (FRECSYS_SIDE_USER / _ITEM: the rows solved by
+ * frecsys_solve_side(side)); the sides differ where a default or
+ * FRECSYS_DUAL_MAX_H_USER / _ITEM sets them apart (Dp = 512: users 320,
+ * items 256).  0 for another side or with the path off. */
+int32_t frecsys_history_space_max_h_side(const frecsys_ctx* ctx, int32_t side);
 
 /* ---- diagnostics (tests) ----
  * The basis the history-space solve uses for G[side]: G = Q T Q^T with Q

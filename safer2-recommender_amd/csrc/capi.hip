@@ -2510,6 +2510,12 @@ int32_t frecsys_history_space_max_h(const frecsys_ctx* c) {
   return c && c->dual_on && c->Dp >= 64 ? c->dual_max_h : 0;
 }
 
+int32_t frecsys_history_space_max_h_side(const frecsys_ctx* c, int32_t side) {
+  if (!c || !c->dual_on || c->Dp < 64 || (side != FRECSYS_SIDE_USER && side != FRECSYS_SIDE_ITEM))
+    return 0;
+  return c->dual_max_h_side[side];
+}
+
 int frecsys_counter(frecsys_ctx* c, const char* what, int64_t* value) {
   if (!c || !what || !value) return fail(c, FRECSYS_ERR_INVALID, "counter: bad arguments");
   if (!strcmp(what, "hspace_reruns")) {

@@ -37,7 +37,7 @@ EXPORTS = (
     "frecsys_synchronize", "frecsys_timing", "frecsys_timing_reset", "frecsys_debug_basis",
     "frecsys_eval_topk", "frecsys_train_stats", "frecsys_pp_set_rating_index",
     "frecsys_pp_predict", "frecsys_pp_step", "frecsys_debug_diag_factor",
-    "frecsys_history_space_max_h", "frecsys_comm_world", "frecsys_gram_groups",
+    "frecsys_history_space_max_h", "frecsys_history_space_max_h_side", "frecsys_comm_world", "frecsys_gram_groups",
     "frecsys_get_gram_groups", "frecsys_set_gram_groups", "frecsys_get_gramian",
     "frecsys_gram_plan", "frecsys_work", "frecsys_snapshot_residual", "frecsys_counter",
     "frecsys_pp_sync", "frecsys_release_workspaces", "frecsys_pp_get_predictions",
@@ -138,6 +138,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "frecsys_timing": (ctypes.c_int, [P, ctypes.c_char_p, P, P]),
         "frecsys_timing_reset": (ctypes.c_int, [P]),
         "frecsys_history_space_max_h": (I32, [P]),
+        "frecsys_history_space_max_h_side": (I32, [P, I32]),
         "frecsys_comm_world": (ctypes.c_int, [P, P, P, P]),
         "frecsys_gram_groups": (ctypes.c_int, [P, I32, P, P, P, P]),
         "frecsys_get_gram_groups": (ctypes.c_int, [P, I32, P]),
@@ -425,8 +426,10 @@ class Context:
                                           ctypes.byref(e), ctypes.byref(n)))
         return float(f.value), float(b.value), int(e.value), int(n.value)
 
-    def history_space_max_h(self) -> int:
-        return int(self.lib.frecsys_history_space_max_h(self.h))
+    def history_space_max_h(self, side=None) -> int:
+        if side is None:
+            return int(self.lib.frecsys_history_space_max_h(self.h))
+        return int(self.lib.frecsys_history_space_max_h_side(self.h, side))
 
     def timing_reset(self):
         self._check(self.lib.frecsys_timing_reset(self.h))

@@ -278,15 +278,19 @@ def test_every_bucket_filled_and_solved(quirk_data, monkeypatch):
     assert rel_rows(ctx.get_embeddings(fh.SIDE_ITEM), Vo).max() < TOL_ROW
 
 
-@pytest.mark.parametrize("dim,expect", [(32, 0), (64, 224), (256, 224), (512, 256), (1024, 512)])
-def test_default_history_space_threshold(quirk_data, dim, expect):
+@pytest.mark.parametrize("dim,expect,user", [(32, 0, 0), (64, 224, 224), (256, 224, 224),
+                                              (512, 256, 320), (1024, 512, 512)])
+def test_default_history_space_threshold(quirk_data, dim, expect, user):
     """Crossover of the two paths (capi.hip): h_eff <= 224 at Dp <= 256 (the
-    d-space kernel is faster for the TH = 8 bucket there), 256 at Dp = 512,
-    512 at Dp = 1024 (the wide bucket, dual.hip); no history-space path
-    below Dp = 64."""
+    d-space kernel is faster for the TH = 8 bucket there), 256 at Dp = 512
+    (the user side 320: its half-step is d-space bound), 512 at
+    Dp = 1024 (the wide bucket, dual.hip); no history-space path below
+    Dp = 64."""
     nu, ni, up, uc, ip, ic = quirk_data
     ctx, U, V = _ctx(dim, nu, ni, up, uc, ip, ic)
     assert ctx.history_space_max_h() == expect
+    assert ctx.history_space_max_h(fh.SIDE_USER) == user
+    assert ctx.history_space_max_h(fh.SIDE_ITEM) == expect
     ctx.close()
 
 

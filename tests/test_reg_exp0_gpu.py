@@ -57,7 +57,8 @@ def test_reg_exp0_well_conditioned_half_step(monkeypatch, ml1m_csr, dim, side): 
         assert ctx.work("basis_chol")[2] == (basis == "chol")
         assert ctx.counter("hspace_reruns") == 0
         outs[basis] = ctx.get_embeddings(s)
-        max_h = ctx.history_space_max_h()  # 256; 512 at Dp = 1024 (the wide bucket)
+        # users 320 / items 256 at Dp = 512, 512 at Dp = 1024 (the wide bucket)
+        max_h = ctx.history_space_max_h(s)
         X = U if side == "user" else V
         ctx.close()
     G0 = O.gramian(X0)
