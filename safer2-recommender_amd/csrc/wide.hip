@@ -983,12 +983,14 @@ __global__ void __launch_bounds__(64 * NW)
 // HBM, and its panel sums fetch 4 KB per 32x32x32 product -- ~157 GB per
 // launch at config 5, 4.1 TB/s, MFMA busy 0.21.  Here panels p and p+1 are
 // summed together, so every streamed L_Iq feeds two products:
-//   U  waves 0..6 (workers) hold C_Ip^T and C_I,p+1^T for up to 3 tiles
+//   U  waves 0..6 (workers) hold C_Ip^T and C_I,p+1^T for up to NI tiles
 //      I >= p+2 each (more tiles: another pass over q); rows p and p+1 of L
-//      come through LDS in chunks of C2_QC tiles (register-staged one chunk
-//      ahead, one barrier per chunk); L_Iq from the workspace in a 3-deep
-//      register ring.  Wave 7 (the diagonal wave) sums the diagonal block:
-//      A_pp, A_p+1,p, A_p+1,p+1 and the forward-substitution dots r_p, r_p+1.
+//      come through LDS in chunks of QC tiles (LDS-DMA one chunk ahead), and
+//      each chunk is split once into a negated 3-piece bf16 image that every
+//      wave reads as MFMA operands (two barriers per chunk); L_Iq from the
+//      workspace in a RING-deep register ring.  Wave 7 (the diagonal wave)
+//      sums the diagonal block: A_pp, A_p+1,p, A_p+1,p+1 and the
+//      forward-substitution dots r_p, r_p+1.
 //   D  wave 7: L_pp^-1 (diag_factor_inv); | workers: L_Ip = C_Ip^T L_pp^-T;
 //      L_p+1,p (into LDS);                | workers: C_I,p+1 -= L_Ip L_p+1,p^T;
 //      L_p+1,p+1^-1, y_p, y_p+1;          | workers: L_I,p+1.
